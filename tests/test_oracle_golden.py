@@ -1,0 +1,179 @@
+"""Pin the CPU oracle (oracle/ctn_oracle.py) against vectors captured from the
+real reference (tests/golden/make_golden.py).  CPU only."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import ctn_oracle as O
+
+
+def load(name):
+    return np.load(os.path.join(GOLDEN, name))
+
+
+def T(a):
+    return torch.from_numpy(np.array(a))
+
+
+def close(a, b, rtol=1e-5, atol=1e-5):
+    a = a.detach().numpy() if torch.is_tensor(a) else np.asarray(a)
+    np.testing.assert_allclose(a, b, rtol=rtol, atol=atol)
+
+
+def fwd_bwd(fn, inputs, G):
+    ins = [x.clone().requires_grad_(True) for x in inputs]
+    out = fn(*ins)
+    (out * G).sum().backward()
+    return out.detach(), [x.grad for x in ins]
+
+
+@pytest.mark.parametrize("nm", ["gln", "cln"])
+def test_norms(nm):
+    g = load("ops.npz")
+    fn = O.gln if nm == "gln" else O.cln
+    out, (gy, gg, gb) = fwd_bwd(fn, [T(g[f"{nm}.y"]), T(g[f"{nm}.gamma"]), T(g[f"{nm}.beta"])],
+                               T(g[f"{nm}.G"]))
+    close(out, g[f"{nm}.out"])
+    close(gy, g[f"{nm}.gy"], 1e-4, 1e-4)
+    close(gg, g[f"{nm}.ggamma"], 1e-4, 1e-4)
+    close(gb, g[f"{nm}.gbeta"], 1e-4, 1e-4)
+
+
+@pytest.mark.parametrize("L", [20, 16])
+def test_encoder(L):
+    g = load("ops.npz")
+    out, (_, gU) = fwd_bwd(O.encoder, [T(g[f"enc{L}.x"]), T(g[f"enc{L}.U"])], T(g[f"enc{L}.G"]))
+    close(out, g[f"enc{L}.out"])
+    close(gU, g[f"enc{L}.gU"], 1e-4, 1e-4)
+
+
+def test_ola_known_answer():
+    g = load("ops.npz")
+    close(O.overlap_and_add(T(g["ola.kat.sig"]), 2), g["ola.kat.out"], 0, 0)
+    for L, S in ((20, 10), (16, 8), (15, 7), (6, 3)):
+        close(O.overlap_and_add(T(g[f"ola{L}_{S}.sig"]), S), g[f"ola{L}_{S}.out"])
+
+
+@pytest.mark.parametrize("L", [20, 16])
+def test_decoder(L):
+    g = load("ops.npz")
+    out, (gw, gm, gV) = fwd_bwd(lambda w, m, V: O.decoder(w, m, V, L),
+                                [T(g[f"dec{L}.w"]), T(g[f"dec{L}.m"]), T(g[f"dec{L}.V"])],
+                                T(g[f"dec{L}.G"]))
+    close(out, g[f"dec{L}.out"], 1e-5, 1e-4)
+    close(gw, g[f"dec{L}.gw"], 1e-4, 1e-4)
+    close(gm, g[f"dec{L}.gm"], 1e-4, 1e-4)
+    close(gV, g[f"dec{L}.gV"], 1e-4, 1e-3)
+
+
+TB = [(n, c, d) for n in ("gLN", "cLN") for c in (0, 1) for d in (1, 2, 4, 8, 16, 32, 64, 128)]
+
+
+@pytest.mark.parametrize("norm,causal,d", TB)
+def test_temporal_block(norm, causal, d):
+    g = load("tblock.npz")
+    tag = f"tb.{norm}.{causal}.{d}"
+    names = sorted(k[len(tag) + 3:] for k in g.files if k.startswith(tag + ".p:"))
+    cfg = O.Cfg(4, 4, 8, 16, 3, 1, 1, 2, norm, bool(causal))
+    # tblock_fixtures used a bare TemporalBlock; map its names onto block (0, xi)
+    xi = int(np.log2(d))
+    cfg = O.Cfg(4, 4, 8, 16, 3, xi + 1, 1, 2, norm, bool(causal))
+    pre = O.block_prefix(0, xi)
+    params = {pre + n: T(g[tag + ".p:" + n]).clone().requires_grad_(True) for n in names}
+    x = T(g[tag + ".x"]).clone().requires_grad_(True)
+    out = O.temporal_block(cfg, x, params, 0, xi)
+    (out * T(g[tag + ".G"])).sum().backward()
+    close(out, g[tag + ".out"], 1e-5, 1e-4)
+    close(x.grad, g[tag + ".gx"], 1e-4, 1e-4)
+    for n in names:
+        close(params[pre + n].grad, g[tag + ".g:" + n], 1e-4, 2e-4)
+
+
+@pytest.mark.parametrize("C", [2, 3])
+@pytest.mark.parametrize("tag", ["eq", "neq"])
+def test_pit(C, tag):
+    g = load("pit.npz")
+    k = f"pit.C{C}.{tag}"
+    est = T(g[k + ".est"]).clone().requires_grad_(True)
+    loss, max_snr, est_m, reord = O.cal_loss(T(g[k + ".src"]), est, T(g[k + ".len"]))
+    loss.backward()
+    close(loss, g[k + ".loss"], 1e-5, 1e-5)
+    close(max_snr, g[k + ".max_snr"], 1e-5, 1e-5)
+    close(est_m, g[k + ".est_m"], 0, 0)
+    close(reord, g[k + ".reord"], 0, 0)
+    close(est.grad, g[k + ".gest"], 1e-4, 1e-7)
+
+
+def test_sisnr():
+    g = load("sisnr.npz")
+    for c in range(2):
+        close(O.cal_sisnr(g["ref"][c], g["est"][c]), g["sisnr"][c], 1e-10, 1e-10)
+    close(O.cal_sisnri(g["ref"], g["est"], g["mix"]), g["sisnri"], 1e-10, 1e-10)
+
+
+def cfg_of(g):
+    N, L, B, H, P, X, R, C = [int(v) for v in g["cfg"]]
+    return O.Cfg(N, L, B, H, P, X, R, C, str(g["cfg_norm"]), bool(int(g["cfg_causal"])),
+                 str(g["cfg_mask"]))
+
+
+def model_params(g, cfg):
+    if "p:encoder.conv1d_U.weight" in g.files:
+        return {n: T(g["p:" + n]) for n, _ in O.param_shapes(cfg)}
+    return O.init_params(cfg, int(g["seed"]))
+
+
+MODELS = ["model_c1.npz", "model_paper_short.npz", "model_causal_cln.npz", "model_3spk.npz",
+          "model_softmax_pad.npz", "model_bn.npz"]
+
+
+@pytest.mark.parametrize("name", MODELS)
+def test_model(name):
+    g = load(name)
+    cfg = cfg_of(g)
+    params = model_params(g, cfg)
+    est, loss, max_snr, grads = O.fwd_bwd(cfg, params, T(g["mix"]), T(g["src"]), T(g["len"]))
+    scale = float(np.abs(g["est"]).max())
+    close(est, g["est"], 1e-4, 1e-4 * scale)
+    close(loss, g["loss"], 1e-4, 1e-4)
+    close(max_snr, g["max_snr"], 1e-4, 1e-4)
+    for n, _ in O.param_shapes(cfg):
+        gn = float(g["gnorm:" + n])
+        close(grads[n].norm(), gn, 2e-3, 1e-6)
+        close(grads[n].reshape(-1)[:64], g["ghead:" + n], 2e-3, 2e-3 * gn + 1e-7)
+        if "g:" + n in g.files:
+            close(grads[n], g["g:" + n], 2e-3, 2e-3 * gn + 1e-7)
+
+
+def test_model_sisnri_and_reorder():
+    g = load("model_c1.npz")
+    est, reord = g["est"], g["reord"]
+    for b in range(est.shape[0]):
+        v = O.cal_sisnri(g["src"][b], reord[b], g["mix"][b])
+        close(v, g["sisnri"][b], 1e-6, 1e-6)
+
+
+def test_train_step():
+    g = load("model_c1.npz")
+    cfg = cfg_of(g)
+    params = model_params(g, cfg)
+    _, after = O.train_step(cfg, params, T(g["mix"]), T(g["src"]), T(g["len"]))
+    for n, _ in O.param_shapes(cfg):
+        # Adam normalises g/sqrt(g^2): a 1e-3 step on near-zero grads is order-sensitive
+        close(after[n], g["step:" + n], 1e-5, 2e-5)
+
+
+def test_reference_init_semantics():
+    """c1 was initialised by the reference itself: gamma/beta are xavier-normal
+    (conv_tasnet.py:41-43 overwrites :316-317), PReLU alphas 0.25."""
+    g = load("model_c1.npz")
+    cfg = cfg_of(g)
+    for n, shape in O.param_shapes(cfg):
+        p = g["p:" + n]
+        if len(shape) == 1:
+            assert np.all(p == 0.25), n
+        elif n.endswith("gamma"):
+            assert not np.allclose(p, 1.0), n
