@@ -1,0 +1,149 @@
+// Common device helpers for the Conv-TasNet HIP kernels (gfx950 / CDNA4 only).
+//
+// Storage convention: every frame-major activation is a row
+// matrix [M*Kp][C] — utterance-major, frame rows padded to Kp (a multiple of
+// 128) so that no GEMM row tile straddles two utterances, channels contiguous.
+// Padded rows (k >= K inside an utterance) are kept at zero by every kernel
+// that writes a row tensor.  Storage type T is float (parity mode) or bf16
+// (throughput mode); all arithmetic, statistics and accumulation are fp32
+// (block/utterance reductions in fp64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define CTN_DEV __device__ __forceinline__
+
+typedef uint16_t bf16raw;
+struct alignas(16) u128 { uint32_t x, y, z, w; };
+
+CTN_DEV float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+CTN_DEV uint16_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
+
+// ---------------------------------------------------------------------------
+// 8-element vector load/store in fp32 registers for either storage type.
+// bf16: one 16-byte access; f32: two 16-byte accesses.
+// ---------------------------------------------------------------------------
+template <typename T> struct Vec8;
+
+template <> struct Vec8<float> {
+  static CTN_DEV void load(const float* p, float v[8]) {
+    const float4 a = *reinterpret_cast<const float4*>(p);
+    const float4 b = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  static CTN_DEV void store(float* p, const float v[8]) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+};
+
+template <> struct Vec8<bf16raw> {
+  static CTN_DEV void load(const bf16raw* p, float v[8]) {
+    const u128 a = *reinterpret_cast<const u128*>(p);
+    const uint32_t w[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(w[i] << 16);
+      v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+  static CTN_DEV void store(bf16raw* p, const float v[8]) {
+    u128 a;
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
+    a.x = w[0]; a.y = w[1]; a.z = w[2]; a.w = w[3];
+    *reinterpret_cast<u128*>(p) = a;
+  }
+};
+
+// 4-element store (GEMM epilogue: one lane owns 4 consecutive output columns)
+template <typename T> CTN_DEV void store4(T* p, const float v[4]);
+template <> CTN_DEV void store4<float>(float* p, const float v[4]) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+}
+template <> CTN_DEV void store4<bf16raw>(bf16raw* p, const float v[4]) {
+  uint2 a;
+  a.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+  a.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+  *reinterpret_cast<uint2*>(p) = a;
+}
+template <typename T> CTN_DEV void load4(const T* p, float v[4]);
+template <> CTN_DEV void load4<float>(const float* p, float v[4]) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+}
+template <> CTN_DEV void load4<bf16raw>(const bf16raw* p, float v[4]) {
+  const uint2 a = *reinterpret_cast<const uint2*>(p);
+  v[0] = __uint_as_float(a.x << 16); v[1] = __uint_as_float(a.x & 0xffff0000u);
+  v[2] = __uint_as_float(a.y << 16); v[3] = __uint_as_float(a.y & 0xffff0000u);
+}
+
+template <typename T> CTN_DEV float ld1(const T* p);
+template <> CTN_DEV float ld1<float>(const float* p) { return *p; }
+template <> CTN_DEV float ld1<bf16raw>(const bf16raw* p) { return bf2f(*p); }
+template <typename T> CTN_DEV void st1(T* p, float v);
+template <> CTN_DEV void st1<float>(float* p, float v) { *p = v; }
+template <> CTN_DEV void st1<bf16raw>(bf16raw* p, float v) { *p = f2bf(v); }
+
+// ---------------------------------------------------------------------------
+// activations
+// ---------------------------------------------------------------------------
+// nn.PReLU with one shared alpha: max(0,x) + a*min(0,x)  (conv_tasnet.py:218,253)
+CTN_DEV float prelu(float x, float a) { return x > 0.f ? x : a * x; }
+// d prelu / dx, with torch's convention at x == 0 (slope a)
+CTN_DEV float prelu_dx(float x, float a) { return x > 0.f ? 1.f : a; }
+// d prelu / da
+CTN_DEV float prelu_da(float x) { return x > 0.f ? 0.f : x; }
+
+// ---------------------------------------------------------------------------
+// wave64 / block reductions
+// ---------------------------------------------------------------------------
+template <typename V> CTN_DEV V wave_sum(V v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+// sum over lanes that share (lane % width) == const, i.e. reduce across lane / width groups
+template <typename V> CTN_DEV V wave_sum_stride(V v, int width) {
+  for (int o = 32; o >= width; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+// sum over aligned lane groups of size `width` (power of two <= 64)
+template <typename V> CTN_DEV V wave_sum_group(V v, int width) {
+  for (int o = width >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Block-wide sum of NV doubles; result valid in thread 0.  `red` must hold
+// NV * (blockDim.x / 64) doubles.  Contains __syncthreads().
+template <int NV> CTN_DEV void block_sum_d(double (&v)[NV], double* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) v[i] = wave_sum(v[i]);
+  if (lane == 0)
+#pragma unroll
+    for (int i = 0; i < NV; ++i) red[wid * NV + i] = v[i];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < nw; ++w)
+#pragma unroll
+      for (int i = 0; i < NV; ++i) v[i] += red[w * NV + i];
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// normalisation statistics: layout shared by all kernels
+//   gLN : one (mean, rstd) pair per utterance       index = m
+//   cLN : one (mean, rstd) pair per padded frame row index = row
+// ---------------------------------------------------------------------------
+enum NormKind { NORM_GLN = 0, NORM_CLN = 1 };
+
+template <int NK> CTN_DEV int stat_index(int row, int Kp) {
+  return NK == NORM_GLN ? row / Kp : row;
+}
+
+static inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }

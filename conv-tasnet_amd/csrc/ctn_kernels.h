@@ -1,0 +1,116 @@
+// Internal (C++) launcher interface between the kernel files and the C-ABI
+// layer (ctn_capi.hip).  Not part of the public ABI: see include/ctn.h.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace ctn {
+
+enum DType { F32 = 0, BF16 = 1 };
+enum RowOpKind { OP_PLAIN = 0, OP_NORM = 1, OP_PRELU_NORM = 2 };
+enum EpiKind { EPI_STORE = 0, EPI_PRELU_STATS = 1, EPI_RESID = 2, EPI_NORM_BWD = 3 };
+
+// element-wise transform applied to an operand row while it is staged into LDS
+struct RowOp {
+  int kind = OP_PLAIN;       // RowOpKind
+  int norm = 0;              // NormKind of `stats` (0 gLN per utterance, 1 cLN per row)
+  const float2* stats = nullptr;   // (mean, rstd)
+  const float* gamma = nullptr;
+  const float* beta = nullptr;
+  const float* alpha = nullptr;    // PReLU alpha (device pointer, 1 element)
+};
+
+// Geometry of a frame-row tensor set: rows = M * Kp, valid frames K per utterance.
+struct Rows {
+  int M, K, Kp;
+  __host__ __device__ long rows() const { return (long)M * Kp; }
+};
+
+// ---- row GEMM:  C[r][n] = sum_k op(A[r][k]) * W[n][k]  (+ epilogue) ---------
+struct GemmRows {
+  Rows g;
+  int Kred, Nout;
+  const void* A; int lda;
+  const void* W; int ldw;      // [Nout][Kred], storage type
+  RowOp aop;
+  int epi = EPI_STORE;
+  void* C; int ldc;
+  const void* R = nullptr; int ldr = 0;   // residual (EPI_RESID) or pre-activation (EPI_NORM_BWD)
+  const float* alpha = nullptr;           // PReLU alpha for the epilogue
+  const float2* stats = nullptr;          // EPI_NORM_BWD forward stats
+  const float* gamma = nullptr;           // EPI_NORM_BWD gamma
+  int norm = 0;                           // NormKind for the epilogue statistics
+  double2* grp_slab = nullptr;            // group partials
+  float* col_slab = nullptr;              // EPI_NORM_BWD column partials [rowtiles][2][Nout]
+};
+int gemm_rows_tiles_per_group(const GemmRows& p);   // slab parts per group
+int gemm_rows_rowtiles(const GemmRows& p);
+hipError_t launch_gemm_rows(DType dt, const GemmRows& p, hipStream_t s);
+
+// ---- column GEMM (weight gradient): Cpart[chunk][p][q] = sum_r opA(A[r][p]) * opB(B[r][q])
+struct GemmCols {
+  Rows g;
+  int P, Q;
+  const void* A; int lda; RowOp aop;
+  const void* B; int ldb; RowOp bop;
+  float* Cpart;                // [nchunks][P][Q]
+  int nchunks;
+};
+int gemm_cols_default_chunks(const GemmCols& p);
+hipError_t launch_gemm_cols(DType dt, const GemmCols& p, hipStream_t s);
+
+// ---- statistics ------------------------------------------------------------
+// slab: [G][nparts] double2 partials -> out[G] float2
+//   mode 0: (mean, rstd) with biased variance, eps inside the sqrt
+//   mode 1: (S1 / cnt, S2 / cnt)
+hipError_t launch_stats_finalize(const double2* slab, int G, int nparts, double cnt, int mode,
+                                 float eps, float2* out, hipStream_t s);
+
+struct SlabDesc {
+  const float* src;   // parts laid out with stride `pstride` floats
+  float* dst;
+  int nparts, n, pstride;
+};
+struct SlabBatch {
+  SlabDesc d[12];
+  int nd;
+};
+hipError_t launch_slab_reduce(const SlabBatch& b, hipStream_t s);
+
+// fp32 weight [O][I] -> storage-type copy (Ws, [O][I]) and/or transpose (Wt, [I][O])
+hipError_t launch_prep_weight(DType dt, const float* W, int O, int I, void* Ws, void* Wt,
+                              hipStream_t s);
+
+// ---- depthwise + norm element-wise kernels ---------------------------------
+struct DwArgs {
+  Rows g;
+  int H, P, dil, pad;
+  int norm;                              // NormKind of both block norms
+  const void* h1;                        // pre-PReLU output of the block's first 1x1 conv
+  const void* d;                         // pre-PReLU output of the depthwise conv (bwd)
+  const float2* st1; const float2* st2;  // forward (mean, rstd)
+  const float* alpha1; const float* gamma1; const float* beta1;
+  const float* alpha2; const float* gamma2;
+  const float* wd;                       // [H][P]
+  // fwd
+  void* d_out;
+  double2* slab2;                        // stats partial of prelu(d)
+  // bwd
+  const void* ga2;                       // dL/d(hat a2) = g_n2 * gamma2
+  const float2* sm2;                     // (mean ga2, mean ga2*hat a2)
+  void* ga1_out;                         // dL/d(hat a1)
+  double2* slab1;                        // partial (S1, S2) of layer-1 norm backward
+  float* col_slab;                       // [blocks][H*(2+P)+4]: ggamma1, gbeta1, gwd, galpha2
+  const float2* sm1;                     // (ew) layer-1 sums
+  void* gh1_out;                         // (ew) dL/dh1
+  float* alpha_slab;                     // (ew) [blocks] galpha1 partials
+};
+int dw_blocks(const DwArgs& a);
+int dw_parts_per_group(const DwArgs& a);   // slab parts per utterance (gLN) or per row (cLN)
+__host__ __device__ int dw_col_stride(const DwArgs& a);
+hipError_t launch_dw_fwd(DType dt, const DwArgs& a, hipStream_t s);
+hipError_t launch_dw_bwd(DType dt, const DwArgs& a, hipStream_t s);
+hipError_t launch_norm1_bwd(DType dt, const DwArgs& a, hipStream_t s);
+
+}  // namespace ctn

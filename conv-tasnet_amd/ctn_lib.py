@@ -1,0 +1,136 @@
+"""ctypes binding of libctn_hip.so (include/ctn.h).
+
+The shared library is the product: every forward/backward of the drop-in
+modules runs through it.  Loading is lazy; a missing or unloadable library
+raises ``CtnLibraryError`` — there is no fallback path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("CTN_HIP_LIB", os.path.join(_HERE, "libctn_hip.so"))
+ABI_VERSION = 1
+
+DTYPE_F32, DTYPE_BF16 = 0, 1
+NORM_GLN, NORM_CLN = 0, 1
+MASK_RELU, MASK_SOFTMAX = 0, 1
+ROW_TILE = 128
+
+c_int32, c_void_p, c_size_t = ctypes.c_int32, ctypes.c_void_p, ctypes.c_size_t
+
+
+class CtnLibraryError(RuntimeError):
+    """libctn_hip.so is missing, stale or failed a call."""
+
+
+# ----------------------------------------------------------------------------
+# C structs (mirror include/ctn.h)
+# ----------------------------------------------------------------------------
+class TBlockDesc(ctypes.Structure):
+    _fields_ = [(n, c_int32) for n in
+                ("M", "K", "Kp", "B", "H", "P", "dilation", "causal", "norm_type", "dtype")]
+
+
+_TB_PARAM_NAMES = ("w1", "alpha1", "gamma1", "beta1", "wd", "alpha2", "gamma2", "beta2", "w2")
+
+
+class TBlockParams(ctypes.Structure):
+    _fields_ = [(n, c_void_p) for n in _TB_PARAM_NAMES]
+
+
+class TBlockGrads(ctypes.Structure):
+    _fields_ = [(n, c_void_p) for n in _TB_PARAM_NAMES]
+
+
+class TBlockSaved(ctypes.Structure):
+    _fields_ = [("h1", c_void_p), ("d", c_void_p), ("stats", c_void_p)]
+
+
+# ----------------------------------------------------------------------------
+_lib = None
+_lock = threading.Lock()
+
+_SIGS = {
+    "ctn_abi_version": (ctypes.c_int, []),
+    "ctn_last_error": (ctypes.c_char_p, []),
+    "ctn_padded_frames": (ctypes.c_int, [ctypes.c_int]),
+    "ctn_tblock_stats_floats": (ctypes.c_int, [c_void_p]),
+    "ctn_tblock_workspace_bytes": (c_size_t, [c_void_p, ctypes.c_int]),
+    "ctn_tblock_forward": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                          c_void_p, c_size_t, c_void_p]),
+    "ctn_tblock_backward": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                           c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "ctn_timer_enable": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    "ctn_timer_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
+}
+
+EXPORTED_SYMBOLS = tuple(_SIGS)
+
+
+def load(path: str = LIB_PATH):
+    """Load (once) and return the CDLL; raises CtnLibraryError if unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise CtnLibraryError(
+                f"HIP extension not built: {path} is missing (run `make` or "
+                f"`python -c 'import __graft_entry__ as g; g.build()'`)")
+        try:
+            lib = ctypes.CDLL(path)
+        except OSError as e:
+            raise CtnLibraryError(f"cannot load {path}: {e}") from e
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        v = lib.ctn_abi_version()
+        if v != ABI_VERSION:
+            raise CtnLibraryError(f"{path} has ABI {v}, expected {ABI_VERSION}; rebuild")
+        _lib = lib
+        return lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = load().ctn_last_error().decode(errors="replace")
+        raise CtnLibraryError(f"{what} failed (status {rc}): {msg}")
+
+
+def padded_frames(K: int) -> int:
+    return ((K + ROW_TILE - 1) // ROW_TILE) * ROW_TILE
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def stream_handle(device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    if dt == torch.float32:
+        return DTYPE_F32
+    if dt == torch.bfloat16:
+        return DTYPE_BF16
+    raise CtnLibraryError(f"unsupported activation dtype {dt} (float32 or bfloat16)")
+
+
+def workspace(nbytes: int, device) -> torch.Tensor:
+    return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+
+
+def require_device(t: torch.Tensor, what: str):
+    if not t.is_cuda:
+        raise CtnLibraryError(
+            f"{what}: the MI355X build runs on a ROCm device only (got a {t.device} tensor); "
+            f"the CPU restatement in oracle/ is test infrastructure, not a fallback")

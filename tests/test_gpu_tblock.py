@@ -1,0 +1,108 @@
+"""TemporalBlock HIP path (ctn_tblock_forward/backward) vs the reference's
+golden vectors and vs the CPU oracle.  GPU only."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import ctn_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _names(causal):
+    off = 1 if causal else 0
+    return ["net.0.weight", "net.1.weight", "net.2.gamma", "net.2.beta", "net.3.net.0.weight",
+            f"net.3.net.{1 + off}.weight", f"net.3.net.{2 + off}.gamma", f"net.3.net.{2 + off}.beta",
+            f"net.3.net.{3 + off}.weight"]
+
+
+def run_block(x_ncw, params, P, dil, causal, norm, G_ncw, dtype=torch.float32):
+    import ctn_ops as ops
+    import ctn_lib as L
+    M, B, K = x_ncw.shape
+    H = params[0].shape[0]
+    fr = ops.Frames.of(M, K)
+    x = ops.ncw_to_rows(x_ncw.to(DEV), fr, dtype).requires_grad_(True)
+    ps = [p.to(DEV).float().clone().requires_grad_(True) for p in params]
+    cfg = (B, H, P, dil, causal, L.NORM_GLN if norm == "gLN" else L.NORM_CLN)
+    y = ops.TBlockFn.apply(x, fr, cfg, *ps)
+    y_ncw = ops.rows_to_ncw(y, fr, torch.float32)
+    (y_ncw * G_ncw.to(DEV)).sum().backward()
+    gx = ops.rows_to_ncw(x.grad, fr, torch.float32)
+    return y_ncw.detach().cpu(), gx.detach().cpu(), [p.grad.detach().cpu() for p in ps], y, x
+
+
+def rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
+
+
+TB = [(n, c, d) for n in ("gLN", "cLN") for c in (0, 1) for d in (1, 2, 4, 8, 16, 32, 64, 128)]
+
+
+@pytest.mark.parametrize("norm,causal,d", TB)
+def test_tblock_golden_f32(norm, causal, d):
+    g = np.load(os.path.join(GOLDEN, "tblock.npz"))
+    tag = f"tb.{norm}.{causal}.{d}"
+    names = _names(causal)
+    params = [torch.from_numpy(g[tag + ".p:" + n]) for n in names]
+    y, gx, gp, yrows, _ = run_block(torch.from_numpy(g[tag + ".x"]), params, 3, d, causal, norm,
+                                    torch.from_numpy(g[tag + ".G"]))
+    # tolerance: fp32 everywhere, different summation order than the reference
+    np.testing.assert_allclose(y.numpy(), g[tag + ".out"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(gx.numpy(), g[tag + ".gx"], rtol=1e-4, atol=2e-4)
+    for n, gg in zip(names, gp):
+        ref = g[tag + ".g:" + n]
+        scale = np.abs(ref).max() + 1e-6
+        np.testing.assert_allclose(gg.numpy().reshape(ref.shape), ref, rtol=1e-3, atol=1e-4 * scale + 1e-5,
+                                   err_msg=n)
+    # padded rows stay zero
+    fr_rows = yrows.view(1, -1, yrows.shape[1])
+    assert torch.count_nonzero(fr_rows[:, 301:]) == 0
+
+
+def _paper_block(seed, B=256, H=512, causal=False, norm="gLN"):
+    rng = np.random.default_rng(seed)
+    P = 3
+    shapes = [(H, B, 1), (1,), (1, H, 1), (1, H, 1), (H, 1, P), (1,), (1, H, 1), (1, H, 1), (B, H, 1)]
+    out = []
+    for s in shapes:
+        if s == (1,):
+            out.append(torch.tensor([0.25 + 0.1 * rng.standard_normal()], dtype=torch.float32))
+        else:
+            out.append(torch.from_numpy((rng.standard_normal(s) * O.xavier_normal_std(s)).astype(np.float32)))
+    return out
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-4), (torch.bfloat16, 3e-2)])
+@pytest.mark.parametrize("d,causal,norm", [(1, 0, "gLN"), (128, 0, "gLN"), (16, 1, "cLN")])
+def test_tblock_paper_dims_vs_oracle(dtype, tol, d, causal, norm):
+    """Paper dims (B=256, H=512), 2 utterances of K=3199 frames: multi-tile GEMMs,
+    chunked weight-gradient GEMMs, all vs the fp32 CPU oracle."""
+    torch.manual_seed(0)
+    params = _paper_block(1, causal=bool(causal), norm=norm)
+    M, B, K = 2, 256, 3199
+    x = torch.randn(M, B, K)
+    G = torch.randn(M, B, K)
+    y, gx, gp, _, _ = run_block(x, params, 3, d, causal, norm, G, dtype)
+    cfg = O.Cfg(4, 4, B, 512, 3, int(np.log2(d)) + 1, 1, 2, norm, bool(causal))
+    xi = int(np.log2(d))
+    names = [O.block_prefix(0, xi) + n for n in _names(causal)]
+    pd = {n: p.clone().requires_grad_(True) for n, p in zip(names, params)}
+    xr = x.clone().requires_grad_(True)
+    yr = O.temporal_block(cfg, xr, pd, 0, xi)
+    (yr * G).sum().backward()
+    assert rel(y, yr.detach()) < tol
+    assert rel(gx, xr.grad) < tol
+    for n, gg in zip(names, gp):
+        if dtype == torch.bfloat16 and pd[n].numel() == 1:
+            # dL/d alpha = sum over M*K*H terms of dL/da * min(x, 0); the per-frame norm
+            # backward makes it a heavily cancelling sum, so bf16-stored operands leave
+            # O(1) relative noise in it.  Its fp32 parity is checked above (dtype=f32).
+            continue
+        assert rel(gg.reshape(pd[n].shape), pd[n].grad) < tol * 5, n
