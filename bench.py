@@ -1,0 +1,213 @@
+#!/usr/bin/env python3
+"""Conv-TasNet training-step throughput on MI355X (BASELINE.json metric).
+
+One step = forward + PIT SI-SNR loss + backward + clip_grad_norm_(5) + Adam
+(src/solver.py:178-186) over one per-GPU batch of synthetic speech-like
+mixtures already resident in HBM.  Workload: paper config (N=256 L=20 B=256
+H=512 P=3 X=8 R=4 gLN, 2 speakers, 4 s @ 8 kHz), 32 utterances per GPU, bf16
+activations (fp32 params/stats/accumulation).  N GPUs = one process per GPU
+under torchrun, DDP over RCCL (weak scaling: per-GPU batch fixed).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+Prints ONE JSON line (rank 0).  `roofline` is measured live: the dominant
+kernel's launches inside the timed region are bracketed by hipEvents on their
+own stream (ctn_timer_*), and achieved = algorithmic bytes per launch / mean
+launch time.  `cpu_baseline` times the fp32 CPU oracle (oracle/, test
+infrastructure — never part of the GPU path) on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "conv-tasnet_amd"))
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+BF16_PEAK_TFLOPS = 2500.0      # dense bf16 MFMA
+
+PAPER = dict(N=256, L=20, B=256, H=512, P=3, X=8, R=4, C=2, norm_type="gLN", causal=False,
+             mask_nonlinear="relu")
+
+# timer kinds (include/ctn.h ctn_timer_enable)
+TIMER_GEMM1, TIMER_DW_FWD, TIMER_GEMM_BWD_A = 1, 2, 3
+
+
+def kernel_bytes(kind, M, K, cfg, s=2):
+    """Algorithmic HBM bytes per launch of the timed kernel family."""
+    B, H = cfg["B"], cfg["H"]
+    rows = M * K
+    if kind == TIMER_GEMM1:        # x[B] in, h1[H] out, W1 once
+        return rows * (B + H) * s + B * H * s
+    if kind == TIMER_DW_FWD:       # h1[H] in, d[H] out
+        return rows * 2 * H * s
+    if kind == TIMER_GEMM_BWD_A:   # gy[B] in, d[H] in, g[H] out, W2t once
+        return rows * (B + 2 * H) * s + B * H * s
+    raise ValueError(kind)
+
+
+def step_alg_bytes(M, K, T, cfg, s=2):
+    """SURVEY.md §8(d) compulsory bytes of one fwd+bwd step: X*R*(12H+7B)*K*s + edges."""
+    N, B, H, C, X, R = cfg["N"], cfg["B"], cfg["H"], cfg["C"], cfg["X"], cfg["R"]
+    per_utt = X * R * (12 * H + 7 * B) * K * s + (3 * N * K + 3 * B * K + 6 * C * N * K + 3 * C * T + 2 * T) * s
+    return M * per_utt
+
+
+def step_flops(M, K, cfg):
+    N, L, B, H, P, X, R, C = (cfg[k] for k in ("N", "L", "B", "H", "P", "X", "R", "C"))
+    f = 2 * K * (N * L + N * B + X * R * (2 * B * H + H * P) + B * C * N + C * N * L)
+    return 3 * f * M
+
+
+def cpu_baseline(seconds=15.0):
+    """fp32 CPU oracle train step (fwd + loss + bwd + clip + Adam) on the paper config, M=1."""
+    from oracle import ctn_oracle as O
+    import synthetic
+    cfg = O.Cfg(**{k: PAPER[k] for k in ("N", "L", "B", "H", "P", "X", "R", "C")})
+    params = O.init_params(cfg, 0)
+    mix, src = synthetic.speech_like(1, cfg.C, 32000, 99)
+    lens = torch.tensor([32000])
+    O.train_step(cfg, params, mix, src, lens)                 # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        _, params = O.train_step(cfg, params, mix, src, lens)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": n / el, "unit": "utterances/sec", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"{n} training steps (fwd+PIT loss+bwd+clip+Adam) of 1 utterance, paper config, "
+                      f"4 s @ 8 kHz, fp32 oracle/ctn_oracle.py, {el:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32, help="utterances per GPU")
+    ap.add_argument("--seconds", type=float, default=4.0)
+    ap.add_argument("--fp32", action="store_true", help="fp32 activations (parity mode) instead of bf16")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--timer-kind", type=int, default=TIMER_GEMM_BWD_A)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    import conv_tasnet as ct
+    import ctn_lib as L
+    import pit_criterion as pc
+    import synthetic
+
+    cfg = PAPER
+    M, C = args.batch, cfg["C"]
+    T = int(args.seconds * 8000)
+    K = (T - cfg["L"]) // (cfg["L"] // 2) + 1
+
+    torch.manual_seed(0)
+    model = ct.ConvTasNet(**cfg).to(dev)
+    model.act_dtype = torch.float32 if args.fp32 else torch.bfloat16
+    if world > 1:
+        model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], bucket_cap_mb=25)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
+    mix, src = synthetic.speech_like(M, C, T, 1234 + rank)
+    mix, src = mix.to(dev), src.to(dev)
+    lens = torch.full((M,), T, dtype=torch.int64, device=dev)
+
+    def step():
+        est = model(mix)
+        loss = pc.cal_loss(src, est, lens)[0]
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 5.0)
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    lib = L.load()
+    L.check(lib.ctn_timer_enable(args.timer_kind, args.steps * 64), "ctn_timer_enable")
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    tot = ctypes.c_double(0.0)
+    nl = ctypes.c_int(0)
+    L.check(lib.ctn_timer_read(ctypes.byref(tot), ctypes.byref(nl)), "ctn_timer_read")
+    lib.ctn_timer_enable(0, 0)
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    final_loss = float(loss)
+
+    if rank == 0:
+        s = 4 if args.fp32 else 2
+        ms = elapsed / args.steps * 1e3
+        utt_s = world * M * args.steps / elapsed
+        kb = kernel_bytes(args.timer_kind, M, K, cfg, s)
+        mean_ms = tot.value / max(nl.value, 1)
+        achieved = kb / (mean_ms * 1e-3) / 1e9
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                traffic = json.load(f).get(str(args.timer_kind))
+        out = {
+            "metric": "utterances/sec (4s, 8kHz, 2-spk) fwd+bwd",
+            "value": round(utt_s, 2),
+            "unit": "utterances/sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32" if args.fp32 else "bf16",
+            "data": "synthetic (AR(2) speech-like sources, random-init weights)",
+            "config": {"workload": "paper config train step c2: N=256 L=20 B=256 H=512 P=3 X=8 R=4 gLN "
+                                   "non-causal relu-mask, 2 spk, 4 s @ 8 kHz, fwd+PIT loss+bwd+clip+Adam",
+                       "per_gpu_batch": M, "global_batch": M * world, "samples": T, "frames": K,
+                       "parallelism": f"dp{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": {1: "gemm_rows fwd 1x1 B->H (PReLU-stats epilogue)",
+                                    2: "dw_fwd (norm1+depthwise+stats)",
+                                    3: "gemm_rows bwd g_n2 = gy.W2 (norm-backward epilogue)"}[args.timer_kind],
+                         "launches": nl.value, "mean_ms": round(mean_ms, 4), "bytes_per_launch": kb},
+            "step_model": {"alg_bytes_GB": round(step_alg_bytes(M, K, T, cfg, s) / 1e9, 3),
+                           "alg_GBps": round(step_alg_bytes(M, K, T, cfg, s) / (ms * 1e-3) / 1e9, 1),
+                           "tflops": round(step_flops(M, K, cfg) / (ms * 1e-3) / 1e12, 1)},
+            "final_loss": round(final_loss, 4),
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,320 @@
+"""Drop-in for jwr1995/Conv-TasNet ``src/conv_tasnet.py`` on MI355X.
+
+Same classes, constructor signatures, attributes, submodule tree, parameter
+names/shapes/order and init as the reference, so
+``from conv_tasnet import ConvTasNet`` with ``PYTHONPATH=conv-tasnet_amd``
+replaces the reference import (src/train.py:12, evaluate.py:16, separate.py:14)
+and reference checkpoints load unchanged.  ``forward`` runs the hand-written
+HIP kernels of ``libctn_hip.so`` (include/ctn.h) on a ROCm device:
+
+    EncoderFn  : encoder + separator cLN + bottleneck        (one native call)
+    TBlockFn   : each of the R*X TemporalBlocks               (one native call)
+    DecoderFn  : mask conv + nonlinearity + decoder + OLA/pad (one native call)
+
+Activation dtype: float32, or bfloat16 when the forward runs under
+``torch.autocast("cuda", dtype=torch.bfloat16)`` (statistics, accumulation and
+parameters stay fp32).  CPU tensors raise: there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+import ctn_lib as L
+import ctn_ops as ops
+
+EPS = 1e-8   # conv_tasnet.py:10 (used by the kernels)
+
+
+def _act_dtype(explicit=None):
+    if explicit is not None:
+        return explicit
+    if torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16:
+        return torch.bfloat16
+    return torch.float32
+
+
+def _norm_code(norm_type):
+    if norm_type == "gLN":
+        return L.NORM_GLN
+    if norm_type == "cLN":
+        return L.NORM_CLN
+    raise L.CtnLibraryError(f"norm_type {norm_type!r} (BatchNorm) is not implemented by the HIP path")
+
+
+def _mask_code(mask_nonlinear):
+    if mask_nonlinear == "softmax":
+        return L.MASK_SOFTMAX
+    if mask_nonlinear == "relu":
+        return L.MASK_RELU
+    raise ValueError("Unsupported mask non-linear function")      # conv_tasnet.py:207-208
+
+
+class ConvTasNet(nn.Module):
+    def __init__(self, N, L, B, H, P, X, R, C, norm_type="gLN", causal=False,
+                 mask_nonlinear='relu'):
+        """conv_tasnet.py:14-43 — same arguments, attributes, submodules and init."""
+        super(ConvTasNet, self).__init__()
+        self.N, self.L, self.B, self.H, self.P, self.X, self.R, self.C = N, L, B, H, P, X, R, C
+        self.norm_type = norm_type
+        self.causal = causal
+        self.mask_nonlinear = mask_nonlinear
+        self.encoder = Encoder(L, N)
+        self.separator = TemporalConvNet(N, B, H, P, X, R, C, norm_type, causal, mask_nonlinear)
+        self.decoder = Decoder(N, L)
+        # conv_tasnet.py:41-43: xavier_normal_ on every param with dim > 1, which also
+        # overwrites the [1,C,1] gLN/cLN gamma/beta
+        for p in self.parameters():
+            if p.dim() > 1:
+                nn.init.xavier_normal_(p)
+        self.act_dtype = None     # None: follow autocast; or torch.float32 / torch.bfloat16
+
+    def forward(self, mixture):
+        """mixture [M, T] -> est_source [M, C, T] (conv_tasnet.py:45-60)."""
+        L.require_device(mixture, "ConvTasNet")
+        _mask_code(self.mask_nonlinear)
+        norm = _norm_code(self.norm_type)
+        dt = _act_dtype(self.act_dtype)
+        M, T = mixture.shape
+        K = (T - self.L) // (self.L // 2) + 1
+        fr = ops.Frames.of(M, K)
+        sep = self.separator
+        cln, bott = sep.network[0], sep.network[1]
+        w_rows, x = ops.EncoderFn.apply(mixture, fr, (self.N, self.L, self.B, self.C), dt,
+                                        self.encoder.conv1d_U.weight, cln.gamma, cln.beta, bott.weight)
+        for blk in sep.blocks():
+            x = blk._forward_rows(x, fr, norm)
+        return ops.DecoderFn.apply(x, w_rows, fr, (T, self.N, self.L, self.B, self.C, _mask_code(self.mask_nonlinear)),
+                                   sep.network[3].weight, self.decoder.basis_signals.weight)
+
+    @classmethod
+    def load_model(cls, path):
+        """conv_tasnet.py:62-67 (maps to CPU; weights-only load)."""
+        package = torch.load(path, map_location=lambda storage, loc: storage, weights_only=True)
+        return cls.load_model_from_package(package)
+
+    @classmethod
+    def load_model_from_package(cls, package):
+        """conv_tasnet.py:69-76."""
+        model = cls(package['N'], package['L'], package['B'], package['H'],
+                    package['P'], package['X'], package['R'], package['C'],
+                    norm_type=package['norm_type'], causal=package['causal'],
+                    mask_nonlinear=package['mask_nonlinear'])
+        model.load_state_dict(package['state_dict'])
+        return model
+
+    @staticmethod
+    def serialize(model, optimizer, epoch, tr_loss=None, cv_loss=None):
+        """conv_tasnet.py:78-94 — identical package keys."""
+        package = {
+            'N': model.N, 'L': model.L, 'B': model.B, 'H': model.H,
+            'P': model.P, 'X': model.X, 'R': model.R, 'C': model.C,
+            'norm_type': model.norm_type, 'causal': model.causal,
+            'mask_nonlinear': model.mask_nonlinear,
+            'state_dict': model.state_dict(),
+            'optim_dict': optimizer.state_dict(),
+            'epoch': epoch
+        }
+        if tr_loss is not None:
+            package['tr_loss'] = tr_loss
+            package['cv_loss'] = cv_loss
+        return package
+
+
+class Encoder(nn.Module):
+    """conv_tasnet.py:97-117: ReLU(Conv1d(1, N, L, stride=L//2, bias=False))."""
+
+    def __init__(self, L, N):
+        super(Encoder, self).__init__()
+        self.L, self.N = L, N
+        self.conv1d_U = nn.Conv1d(1, N, kernel_size=L, stride=L // 2, bias=False)
+        self.act_dtype = None
+
+    def forward(self, mixture):
+        """mixture [M, T] -> mixture_w [M, N, K]."""
+        L.require_device(mixture, "Encoder")
+        M, T = mixture.shape
+        K = (T - self.L) // (self.L // 2) + 1
+        fr = ops.Frames.of(M, K)
+        w_rows, _ = ops.EncoderFn.apply(mixture, fr, (self.N, self.L, 8, 1), _act_dtype(self.act_dtype),
+                                        self.conv1d_U.weight, None, None, None)
+        return ops.rows_to_ncw(w_rows, fr)
+
+
+class Decoder(nn.Module):
+    """conv_tasnet.py:120-142: (w ⊙ mask) · basisᵀ, overlap-add with step L//2."""
+
+    def __init__(self, N, L):
+        super(Decoder, self).__init__()
+        self.N, self.L = N, L
+        self.basis_signals = nn.Linear(N, L, bias=False)
+
+    def forward(self, mixture_w, est_mask):
+        """mixture_w [M, N, K], est_mask [M, C, N, K] -> est_source [M, C, (K-1)*L/2 + L]."""
+        L.require_device(mixture_w, "Decoder")
+        M, N, K = mixture_w.shape
+        C = est_mask.shape[1]
+        fr = ops.Frames.of(M, K)
+        dt = mixture_w.dtype if mixture_w.dtype in (torch.float32, torch.bfloat16) else torch.float32
+        w_rows = ops.ncw_to_rows(mixture_w, fr, dt)
+        m_rows = ops.ncw_to_rows(est_mask.reshape(M, C * N, K), fr, dt)
+        T = (K - 1) * (self.L // 2) + self.L
+        return ops.DecoderFn.apply(m_rows, w_rows, fr, (T, N, self.L, 8, C, L.MASK_IDENTITY), None,
+                                   self.basis_signals.weight)
+
+
+class TemporalConvNet(nn.Module):
+    """conv_tasnet.py:145-209 — same network layout:
+    [cLN(N), Conv1x1 N->B, R x [X x TemporalBlock], Conv1x1 B->C*N]."""
+
+    def __init__(self, N, B, H, P, X, R, C, norm_type="gLN", causal=False,
+                 mask_nonlinear='relu'):
+        super(TemporalConvNet, self).__init__()
+        self.C = C
+        self.mask_nonlinear = mask_nonlinear
+        layer_norm = ChannelwiseLayerNorm(N)
+        bottleneck_conv1x1 = nn.Conv1d(N, B, 1, bias=False)
+        repeats = []
+        for r in range(R):
+            blocks = []
+            for x in range(X):
+                dilation = 2 ** x
+                padding = (P - 1) * dilation if causal else (P - 1) * dilation // 2
+                blocks += [TemporalBlock(B, H, P, stride=1, padding=padding, dilation=dilation,
+                                         norm_type=norm_type, causal=causal)]
+            repeats += [nn.Sequential(*blocks)]
+        temporal_conv_net = nn.Sequential(*repeats)
+        mask_conv1x1 = nn.Conv1d(B, C * N, 1, bias=False)
+        self.network = nn.Sequential(layer_norm, bottleneck_conv1x1, temporal_conv_net, mask_conv1x1)
+        self._norm_type = norm_type
+
+    def blocks(self):
+        for rep in self.network[2]:
+            for blk in rep:
+                yield blk
+
+    def forward(self, mixture_w):
+        """mixture_w [M, N, K] -> est_mask [M, C, N, K] (conv_tasnet.py:192-209)."""
+        raise L.CtnLibraryError(
+            "standalone TemporalConvNet.forward is not exposed by the HIP path yet; "
+            "call ConvTasNet.forward (fused encoder/separator/decoder)")
+
+
+class TemporalBlock(nn.Module):
+    """conv_tasnet.py:212-238: x + DSConv(norm(PReLU(Conv1x1_{B->H}(x))))."""
+
+    def __init__(self, in_channels, out_channels, kernel_size,
+                 stride, padding, dilation, norm_type="gLN", causal=False):
+        super(TemporalBlock, self).__init__()
+        conv1x1 = nn.Conv1d(in_channels, out_channels, 1, bias=False)
+        prelu = nn.PReLU()
+        norm = chose_norm(norm_type, out_channels)
+        dsconv = DepthwiseSeparableConv(out_channels, in_channels, kernel_size,
+                                        stride, padding, dilation, norm_type, causal)
+        self.net = nn.Sequential(conv1x1, prelu, norm, dsconv)
+        self._geo = (in_channels, out_channels, kernel_size, dilation, bool(causal), norm_type)
+        if stride != 1:
+            raise ValueError("TemporalBlock: only stride 1 is used by the reference (conv_tasnet.py:177)")
+
+    def _params(self):
+        ds = self.net[3].net
+        off = 1 if self._geo[4] else 0
+        n1, n2 = self.net[2], ds[2 + off]
+        return (self.net[0].weight, self.net[1].weight, n1.gamma, n1.beta, ds[0].weight,
+                ds[1 + off].weight, n2.gamma, n2.beta, ds[3 + off].weight)
+
+    def _forward_rows(self, x_rows, fr, norm):
+        B, H, P, dil, causal, _ = self._geo
+        return ops.TBlockFn.apply(x_rows, fr, (B, H, P, dil, causal, norm), *self._params())
+
+    def forward(self, x):
+        """x [M, B, K] -> [M, B, K]."""
+        L.require_device(x, "TemporalBlock")
+        M, B, K = x.shape
+        fr = ops.Frames.of(M, K)
+        dt = x.dtype if x.dtype in (torch.float32, torch.bfloat16) else torch.float32
+        y = self._forward_rows(ops.ncw_to_rows(x, fr, dt), fr, _norm_code(self._geo[5]))
+        return ops.rows_to_ncw(y, fr)
+
+
+class DepthwiseSeparableConv(nn.Module):
+    """conv_tasnet.py:241-272 — parameter container of the block's second half.
+    Its compute is fused into the TemporalBlock kernels (ctn_tblock_*)."""
+
+    def __init__(self, in_channels, out_channels, kernel_size,
+                 stride, padding, dilation, norm_type="gLN", causal=False):
+        super(DepthwiseSeparableConv, self).__init__()
+        depthwise_conv = nn.Conv1d(in_channels, in_channels, kernel_size,
+                                   stride=stride, padding=padding,
+                                   dilation=dilation, groups=in_channels,
+                                   bias=False)
+        if causal:
+            chomp = Chomp1d(padding)
+        prelu = nn.PReLU()
+        norm = chose_norm(norm_type, in_channels)
+        pointwise_conv = nn.Conv1d(in_channels, out_channels, 1, bias=False)
+        if causal:
+            self.net = nn.Sequential(depthwise_conv, chomp, prelu, norm, pointwise_conv)
+        else:
+            self.net = nn.Sequential(depthwise_conv, prelu, norm, pointwise_conv)
+
+    def forward(self, x):
+        raise L.CtnLibraryError("DepthwiseSeparableConv runs fused inside TemporalBlock on the HIP path")
+
+
+class Chomp1d(nn.Module):
+    """conv_tasnet.py:275-289.  The HIP depthwise kernel pads on the left only,
+    which is identical to symmetric padding followed by this chomp."""
+
+    def __init__(self, chomp_size):
+        super(Chomp1d, self).__init__()
+        self.chomp_size = chomp_size
+
+    def forward(self, x):
+        return x[:, :, :-self.chomp_size].contiguous()
+
+
+def chose_norm(norm_type, channel_size):
+    """conv_tasnet.py:292-303."""
+    if norm_type == "gLN":
+        return GlobalLayerNorm(channel_size)
+    elif norm_type == "cLN":
+        return ChannelwiseLayerNorm(channel_size)
+    else:
+        return nn.BatchNorm1d(channel_size)
+
+
+class ChannelwiseLayerNorm(nn.Module):
+    """Channel-wise Layer Normalization (cLN), conv_tasnet.py:307-329.
+    Applied inside the fused kernels (per-frame statistics, EPS=1e-8)."""
+
+    def __init__(self, channel_size):
+        super(ChannelwiseLayerNorm, self).__init__()
+        self.gamma = nn.Parameter(torch.Tensor(1, channel_size, 1))
+        self.beta = nn.Parameter(torch.Tensor(1, channel_size, 1))
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        self.gamma.data.fill_(1)
+        self.beta.data.zero_()
+
+    def forward(self, y):
+        raise L.CtnLibraryError("cLN runs fused inside the HIP kernels (EncoderFn / TBlockFn)")
+
+
+class GlobalLayerNorm(nn.Module):
+    """Global Layer Normalization (gLN), conv_tasnet.py:332-355.
+    Applied inside the fused kernels (per-utterance statistics, EPS=1e-8)."""
+
+    def __init__(self, channel_size):
+        super(GlobalLayerNorm, self).__init__()
+        self.gamma = nn.Parameter(torch.Tensor(1, channel_size, 1))
+        self.beta = nn.Parameter(torch.Tensor(1, channel_size, 1))
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        self.gamma.data.fill_(1)
+        self.beta.data.zero_()
+
+    def forward(self, y):
+        raise L.CtnLibraryError("gLN runs fused inside the HIP kernels (TBlockFn)")

@@ -363,3 +363,330 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
   CTN_HIP(launch_slab_reduce(sb, s));
   return CTN_OK;
 }
+
+// ===========================================================================
+// Encoder front: encoder + separator cLN + bottleneck
+// ===========================================================================
+#include "ctn_codec.h"
+
+static int codec_check(const ctn_codec_desc* d, bool need_b) {
+  if (!d) return fail(CTN_ERR_ARG, "null descriptor");
+  if (d->M < 1 || d->T < d->L || d->L < 2 || d->L > 32)
+    return fail(CTN_ERR_UNSUPPORTED, "M=%d T=%d L=%d (need T >= L, 2 <= L <= 32)", d->M, d->T, d->L);
+  const int S = d->L / 2;
+  if (d->K != (d->T - d->L) / S + 1) return fail(CTN_ERR_ARG, "K=%d != (T-L)/(L/2)+1", d->K);
+  if (d->Kp != ctn_padded_frames(d->K)) return fail(CTN_ERR_ARG, "Kp=%d != padded(K)", d->Kp);
+  const int cg = d->N / 8;
+  if (d->N % 8 || cg > 64 || (cg & (cg - 1)))
+    return fail(CTN_ERR_UNSUPPORTED, "N=%d: need N/8 a power of two <= 64", d->N);
+  if (need_b && (d->B % 8 || d->B < 8)) return fail(CTN_ERR_UNSUPPORTED, "B=%d must be a multiple of 8", d->B);
+  if (d->C < 1 || d->C > 4) return fail(CTN_ERR_UNSUPPORTED, "C=%d outside 1..4", d->C);
+  if (d->mask_type < 0 || d->mask_type > 2) return fail(CTN_ERR_ARG, "mask_type %d", d->mask_type);
+  if (d->dtype != CTN_DTYPE_F32 && d->dtype != CTN_DTYPE_BF16) return fail(CTN_ERR_ARG, "dtype %d", d->dtype);
+  return CTN_OK;
+}
+
+static CodecArgs codec_args(const ctn_codec_desc* d) {
+  CodecArgs a{};
+  a.M = d->M; a.T = d->T; a.K = d->K; a.Kp = d->Kp; a.N = d->N; a.L = d->L; a.S = d->L / 2; a.C = d->C;
+  a.mask_type = d->mask_type;
+  return a;
+}
+
+namespace {
+struct EncLayout {
+  void *wbs, *wbt, *gcln;
+  float *gpre, *colE, *slabU, *cpartB;
+  int chunksB, nU, rowblocks;
+  size_t bytes;
+};
+EncLayout enc_layout(const ctn_codec_desc* d, int backward, void* ws) {
+  EncLayout L{};
+  Carver c(ws);
+  const size_t es = esize(d->dtype);
+  const long rows = (long)d->M * d->Kp;
+  if (!backward) {
+    if (d->dtype == CTN_DTYPE_BF16) L.wbs = c.take<void>((size_t)d->B * d->N * es);
+  } else {
+    L.wbt = c.take<void>((size_t)d->B * d->N * es);
+    L.gcln = c.take<void>((size_t)rows * d->N * es);
+    L.gpre = c.take<float>((size_t)rows * d->N * sizeof(float));
+    L.rowblocks = (int)(rows / 128);
+    L.colE = c.take<float>((size_t)L.rowblocks * 2 * d->N * sizeof(float));
+    CodecArgs a = codec_args(d);
+    L.nU = frame_outer_chunks(a);
+    L.slabU = c.take<float>((size_t)L.nU * d->N * d->L * sizeof(float));
+    GemmCols gc{};
+    gc.g = Rows{d->M, d->K, d->Kp}; gc.P = d->B; gc.Q = d->N;
+    L.chunksB = gemm_cols_default_chunks(gc);
+    L.cpartB = c.take<float>((size_t)L.chunksB * d->B * d->N * sizeof(float));
+  }
+  L.bytes = c.off + 256;
+  return L;
+}
+}  // namespace
+
+extern "C" size_t ctn_encoder_workspace_bytes(const ctn_codec_desc* d, int backward) {
+  if (codec_check(d, true) != CTN_OK) return 0;
+  return enc_layout(d, backward, nullptr).bytes;
+}
+
+extern "C" int ctn_encoder_forward(const ctn_codec_desc* d, const float* mixture, const float* U,
+                                   const float* gamma0, const float* beta0, const float* wb, void* w_rows,
+                                   float* cln_stats, void* x0, void* ws, size_t ws_bytes, void* stream) {
+  int rc = codec_check(d, wb != nullptr);
+  if (rc) return rc;
+  if (!mixture || !U || !w_rows) return fail(CTN_ERR_ARG, "null pointer");
+  if (wb && (!gamma0 || !beta0 || !cln_stats || !x0)) return fail(CTN_ERR_ARG, "bottleneck needs gamma0/beta0/stats/x0");
+  const EncLayout Ly = enc_layout(d, 0, ws);
+  if (!ws || ws_bytes < Ly.bytes) return fail(CTN_ERR_WORKSPACE, "workspace %zu < %zu", ws_bytes, Ly.bytes);
+  hipStream_t s = (hipStream_t)stream;
+  const DType dt = d->dtype == CTN_DTYPE_BF16 ? BF16 : F32;
+  CodecArgs a = codec_args(d);
+  a.mixture = mixture; a.U = U; a.w_rows = w_rows; a.cln_stats = reinterpret_cast<float2*>(cln_stats);
+  CTN_HIP(launch_enc_fwd(dt, a, s));
+  if (!wb) return CTN_OK;
+  const void* wbp = wb;
+  if (dt == BF16) {
+    CTN_HIP(launch_prep_weight(dt, wb, d->B, d->N, Ly.wbs, nullptr, s));
+    wbp = Ly.wbs;
+  }
+  GemmRows g{};
+  g.g = Rows{d->M, d->K, d->Kp}; g.Kred = d->N; g.Nout = d->B; g.norm = NORM_CLN;
+  g.A = w_rows; g.lda = d->N;
+  g.aop.kind = OP_NORM; g.aop.norm = NORM_CLN; g.aop.stats = a.cln_stats; g.aop.gamma = gamma0; g.aop.beta = beta0;
+  g.W = wbp; g.ldw = d->N;
+  g.epi = EPI_STORE; g.C = x0; g.ldc = d->B;
+  CTN_HIP(launch_gemm_rows(dt, g, s));
+  return CTN_OK;
+}
+
+extern "C" int ctn_encoder_backward(const ctn_codec_desc* d, const float* mixture, const float* U,
+                                    const float* gamma0, const float* beta0, const float* wb, const void* w_rows,
+                                    const float* cln_stats, const void* g_w_rows, const void* g_x0, float* gU,
+                                    float* ggamma0, float* gbeta0, float* gwb, void* ws, size_t ws_bytes,
+                                    void* stream) {
+  int rc = codec_check(d, g_x0 != nullptr);
+  if (rc) return rc;
+  if (!mixture || !w_rows || !gU) return fail(CTN_ERR_ARG, "null pointer");
+  if (g_x0 && (!wb || !gamma0 || !beta0 || !cln_stats || !ggamma0 || !gbeta0 || !gwb))
+    return fail(CTN_ERR_ARG, "bottleneck backward needs wb/gamma0/beta0/stats and their gradient outputs");
+  const EncLayout Ly = enc_layout(d, 1, ws);
+  if (!ws || ws_bytes < Ly.bytes) return fail(CTN_ERR_WORKSPACE, "workspace %zu < %zu", ws_bytes, Ly.bytes);
+  hipStream_t s = (hipStream_t)stream;
+  const DType dt = d->dtype == CTN_DTYPE_BF16 ? BF16 : F32;
+  const Rows rg{d->M, d->K, d->Kp};
+  CodecArgs a = codec_args(d);
+  a.mixture = mixture; a.U = U; a.w_rows = const_cast<void*>(w_rows);
+  a.cln_stats = const_cast<float2*>(reinterpret_cast<const float2*>(cln_stats));
+  a.gamma0 = gamma0; a.gwdec = g_w_rows; a.gpre = Ly.gpre;
+  SlabBatch sb{};
+  if (g_x0) {
+    CTN_HIP(launch_prep_weight(dt, wb, d->B, d->N, nullptr, Ly.wbt, s));   // [N][B]
+    GemmRows g{};
+    g.g = rg; g.Kred = d->B; g.Nout = d->N;
+    g.A = g_x0; g.lda = d->B; g.W = Ly.wbt; g.ldw = d->B;
+    g.epi = EPI_STORE; g.C = Ly.gcln; g.ldc = d->N;
+    CTN_HIP(launch_gemm_rows(dt, g, s));
+    GemmCols gc{};
+    gc.g = rg; gc.P = d->B; gc.Q = d->N;
+    gc.A = g_x0; gc.lda = d->B;
+    gc.B = w_rows; gc.ldb = d->N;
+    gc.bop.kind = OP_NORM; gc.bop.norm = NORM_CLN; gc.bop.stats = a.cln_stats; gc.bop.gamma = gamma0; gc.bop.beta = beta0;
+    gc.Cpart = Ly.cpartB; gc.nchunks = Ly.chunksB;
+    CTN_HIP(launch_gemm_cols(dt, gc, s));
+    a.gcln = Ly.gcln;
+    a.col_slab = Ly.colE;
+    sb.d[sb.nd++] = SlabDesc{Ly.cpartB, gwb, Ly.chunksB, d->B * d->N, d->B * d->N};
+    sb.d[sb.nd++] = SlabDesc{Ly.colE, ggamma0, Ly.rowblocks, d->N, 2 * d->N};
+    sb.d[sb.nd++] = SlabDesc{Ly.colE + d->N, gbeta0, Ly.rowblocks, d->N, 2 * d->N};
+  }
+  CTN_HIP(launch_enc_bwd_rows(dt, a, s));
+  CodecArgs fo = a;
+  fo.col_slab = Ly.slabU;
+  CTN_HIP(launch_frame_outer(dt, 0, fo, s));
+  sb.d[sb.nd++] = SlabDesc{Ly.slabU, gU, Ly.nU, d->N * d->L, d->N * d->L};
+  CTN_HIP(launch_slab_reduce(sb, s));
+  return CTN_OK;
+}
+
+// ===========================================================================
+// Decoder back: mask conv + nonlinearity + decoder + overlap-add + pad
+// ===========================================================================
+namespace {
+struct DecLayout {
+  void *wms, *wmt, *gscore;
+  float *frames, *slabV, *cpartM;
+  int nV, chunksM;
+  size_t bytes;
+};
+DecLayout dec_layout(const ctn_codec_desc* d, int backward, bool with_mask_conv, void* ws) {
+  DecLayout L{};
+  Carver c(ws);
+  const size_t es = esize(d->dtype);
+  const long rows = (long)d->M * d->Kp;
+  const int CN = d->C * d->N;
+  if (!backward) {
+    if (with_mask_conv && d->dtype == CTN_DTYPE_BF16) L.wms = c.take<void>((size_t)CN * d->B * es);
+    L.frames = c.take<float>((size_t)d->M * d->C * d->Kp * d->L * sizeof(float));
+  } else {
+    CodecArgs a = codec_args(d);
+    L.nV = frame_outer_chunks(a);
+    L.slabV = c.take<float>((size_t)L.nV * d->N * d->L * sizeof(float));
+    if (with_mask_conv) {
+      L.wmt = c.take<void>((size_t)CN * d->B * es);
+      L.gscore = c.take<void>((size_t)rows * CN * es);
+      GemmCols gc{};
+      gc.g = Rows{d->M, d->K, d->Kp}; gc.P = CN; gc.Q = d->B;
+      L.chunksM = gemm_cols_default_chunks(gc);
+      L.cpartM = c.take<float>((size_t)L.chunksM * CN * d->B * sizeof(float));
+    }
+  }
+  L.bytes = c.off + 256;
+  return L;
+}
+}  // namespace
+
+extern "C" size_t ctn_decoder_workspace_bytes(const ctn_codec_desc* d, int backward) {
+  if (codec_check(d, d && d->mask_type != CTN_MASK_IDENTITY) != CTN_OK) return 0;
+  return dec_layout(d, backward, d->mask_type != CTN_MASK_IDENTITY, nullptr).bytes;
+}
+
+extern "C" int ctn_decoder_forward(const ctn_codec_desc* d, const void* x_last, const void* w_rows,
+                                   const float* wm, const float* V, void* score, float* est, void* ws,
+                                   size_t ws_bytes, void* stream) {
+  int rc = codec_check(d, wm != nullptr);
+  if (rc) return rc;
+  if (!x_last || !w_rows || !V || !est) return fail(CTN_ERR_ARG, "null pointer");
+  if ((wm == nullptr) != (d->mask_type == CTN_MASK_IDENTITY))
+    return fail(CTN_ERR_ARG, "wm == NULL exactly when mask_type == CTN_MASK_IDENTITY (standalone Decoder)");
+  if (wm && !score) return fail(CTN_ERR_ARG, "score output required with the mask conv");
+  const DecLayout Ly = dec_layout(d, 0, wm != nullptr, ws);
+  if (!ws || ws_bytes < Ly.bytes) return fail(CTN_ERR_WORKSPACE, "workspace %zu < %zu", ws_bytes, Ly.bytes);
+  hipStream_t s = (hipStream_t)stream;
+  const DType dt = d->dtype == CTN_DTYPE_BF16 ? BF16 : F32;
+  const int CN = d->C * d->N;
+  const void* sc = x_last;
+  if (wm) {
+    const void* wmp = wm;
+    if (dt == BF16) {
+      CTN_HIP(launch_prep_weight(dt, wm, CN, d->B, Ly.wms, nullptr, s));
+      wmp = Ly.wms;
+    }
+    GemmRows g{};
+    g.g = Rows{d->M, d->K, d->Kp}; g.Kred = d->B; g.Nout = CN;
+    g.A = x_last; g.lda = d->B; g.W = wmp; g.ldw = d->B;
+    g.epi = EPI_STORE; g.C = score; g.ldc = CN;
+    CTN_HIP(launch_gemm_rows(dt, g, s));
+    sc = score;
+  }
+  CodecArgs a = codec_args(d);
+  a.w_rows = const_cast<void*>(w_rows); a.score = sc; a.V = V; a.frames = Ly.frames; a.est = est;
+  CTN_HIP(launch_dec_fwd(dt, a, s));
+  return CTN_OK;
+}
+
+extern "C" int ctn_decoder_backward(const ctn_codec_desc* d, const void* x_last, const void* w_rows,
+                                    const float* wm, const float* V, const void* score, const float* g_est,
+                                    void* g_x_last, void* g_w_rows, float* gwm, float* gV, void* ws,
+                                    size_t ws_bytes, void* stream) {
+  int rc = codec_check(d, wm != nullptr);
+  if (rc) return rc;
+  if (!x_last || !w_rows || !V || !g_est || !g_x_last || !g_w_rows || !gV) return fail(CTN_ERR_ARG, "null pointer");
+  if ((wm == nullptr) != (d->mask_type == CTN_MASK_IDENTITY))
+    return fail(CTN_ERR_ARG, "wm == NULL exactly when mask_type == CTN_MASK_IDENTITY (standalone Decoder)");
+  if (wm && (!score || !gwm)) return fail(CTN_ERR_ARG, "score and gwm required with the mask conv");
+  const DecLayout Ly = dec_layout(d, 1, wm != nullptr, ws);
+  if (!ws || ws_bytes < Ly.bytes) return fail(CTN_ERR_WORKSPACE, "workspace %zu < %zu", ws_bytes, Ly.bytes);
+  hipStream_t s = (hipStream_t)stream;
+  const DType dt = d->dtype == CTN_DTYPE_BF16 ? BF16 : F32;
+  const Rows rg{d->M, d->K, d->Kp};
+  const int CN = d->C * d->N;
+  CodecArgs a = codec_args(d);
+  a.w_rows = const_cast<void*>(w_rows); a.score = wm ? score : x_last; a.V = V; a.gest = g_est;
+  a.gscore = wm ? Ly.gscore : g_x_last; a.gwdec_out = g_w_rows;
+  CTN_HIP(launch_dec_bwd(dt, a, s));
+  CodecArgs fo = a;
+  fo.col_slab = Ly.slabV;
+  CTN_HIP(launch_frame_outer(dt, 1, fo, s));
+  SlabBatch sb{};
+  sb.d[sb.nd++] = SlabDesc{Ly.slabV, gV, Ly.nV, d->N * d->L, d->N * d->L};
+  if (wm) {
+    CTN_HIP(launch_prep_weight(dt, wm, CN, d->B, nullptr, Ly.wmt, s));   // [B][CN]
+    GemmRows g{};
+    g.g = rg; g.Kred = CN; g.Nout = d->B;
+    g.A = Ly.gscore; g.lda = CN; g.W = Ly.wmt; g.ldw = CN;
+    g.epi = EPI_STORE; g.C = g_x_last; g.ldc = d->B;
+    CTN_HIP(launch_gemm_rows(dt, g, s));
+    GemmCols gc{};
+    gc.g = rg; gc.P = CN; gc.Q = d->B;
+    gc.A = Ly.gscore; gc.lda = CN; gc.B = x_last; gc.ldb = d->B;
+    gc.Cpart = Ly.cpartM; gc.nchunks = Ly.chunksM;
+    CTN_HIP(launch_gemm_cols(dt, gc, s));
+    sb.d[sb.nd++] = SlabDesc{Ly.cpartM, gwm, Ly.chunksM, CN * d->B, CN * d->B};
+  }
+  CTN_HIP(launch_slab_reduce(sb, s));
+  return CTN_OK;
+}
+
+// ===========================================================================
+// PIT SI-SNR loss
+// ===========================================================================
+static int pit_chunks(int T) {
+  int c = (T + 2047) / 2048;
+  return c < 1 ? 1 : (c > 64 ? 64 : c);
+}
+
+static void pit_perms(PitArgs& a) {
+  int p[4] = {0, 1, 2, 3};
+  a.nperm = 0;
+  // lexicographic order == itertools.permutations(range(C)) (pit_criterion.py:66)
+  do {
+    for (int i = 0; i < a.C; ++i) a.perms[a.nperm][i] = p[i];
+    ++a.nperm;
+    int i = a.C - 2;
+    while (i >= 0 && p[i] >= p[i + 1]) --i;
+    if (i < 0) break;
+    int j = a.C - 1;
+    while (p[j] <= p[i]) --j;
+    int t = p[i]; p[i] = p[j]; p[j] = t;
+    for (int l = i + 1, r = a.C - 1; l < r; ++l, --r) { t = p[l]; p[l] = p[r]; p[r] = t; }
+  } while (true);
+}
+
+extern "C" size_t ctn_pit_workspace_bytes(const ctn_pit_desc* d) {
+  if (!d || d->M < 1 || d->C < 1 || d->C > 4 || d->T < 1) return 0;
+  return (size_t)d->M * pit_chunks(d->T) * pit_nv(d->C) * sizeof(double) + 256;
+}
+
+extern "C" int ctn_pit_forward(const ctn_pit_desc* d, const float* source, float* est, const int64_t* lengths,
+                               float* loss, float* max_snr, int64_t* best_perm, float* reordered, float* coef,
+                               void* ws, size_t ws_bytes, void* stream) {
+  if (!d || d->M < 1 || d->C < 1 || d->T < 1) return fail(CTN_ERR_ARG, "bad PIT descriptor");
+  if (d->C > 4) return fail(CTN_ERR_UNSUPPORTED, "C=%d > 4 speakers", d->C);
+  if (!source || !est || !lengths || !loss || !max_snr || !best_perm || !coef) return fail(CTN_ERR_ARG, "null pointer");
+  if (!ws || ws_bytes < ctn_pit_workspace_bytes(d)) return fail(CTN_ERR_WORKSPACE, "PIT workspace too small");
+  PitArgs a{};
+  a.M = d->M; a.C = d->C; a.T = d->T;
+  a.src = source; a.est = est; a.lengths = lengths;
+  a.slab = reinterpret_cast<double*>(ws);
+  a.chunks = pit_chunks(d->T);
+  a.max_snr = max_snr; a.best = best_perm; a.coef = coef; a.loss = loss;
+  a.est_inplace = est; a.reordered = reordered;
+  pit_perms(a);
+  CTN_HIP(launch_pit_forward(a, (hipStream_t)stream));
+  return CTN_OK;
+}
+
+extern "C" int ctn_pit_backward(const ctn_pit_desc* d, const float* source, const float* est,
+                                const int64_t* lengths, const float* coef, const float* g_loss,
+                                const float* g_max_snr, float* g_est, void* stream) {
+  if (!d || d->M < 1 || d->C < 1 || d->C > 4 || d->T < 1) return fail(CTN_ERR_ARG, "bad PIT descriptor");
+  if (!source || !est || !lengths || !coef || !g_est) return fail(CTN_ERR_ARG, "null pointer");
+  PitArgs a{};
+  a.M = d->M; a.C = d->C; a.T = d->T;
+  a.src = source; a.est = est; a.lengths = lengths; a.coef = const_cast<float*>(coef);
+  a.g_loss = g_loss; a.g_maxsnr = g_max_snr; a.gest = g_est;
+  CTN_HIP(launch_pit_backward(a, (hipStream_t)stream));
+  return CTN_OK;
+}

@@ -1,0 +1,59 @@
+// Internal launcher interface for the encoder/decoder/OLA and PIT kernels.
+#pragma once
+#include "ctn_kernels.h"
+
+namespace ctn {
+
+struct CodecArgs {
+  int M, T, K, Kp, N, L, S, C;
+  int mask_type;                 // 0 relu, 1 softmax over speakers, 2 identity (standalone Decoder)
+  const float* mixture;          // [M][T]
+  const float* U;                // encoder basis [N][L]
+  const float* V;                // decoder basis [L][N]
+  void* w_rows;                  // encoder output [M*Kp][N]
+  float2* cln_stats;             // per-frame (mean, rstd) of w
+  const float* gamma0;           // separator cLN gamma (backward)
+  const void* gcln;              // dL/d cLN(w) rows (backward)
+  const void* gwdec;             // dL/dw from the decoder rows (backward)
+  float* gpre;                   // dL/d(pre-ReLU) rows fp32 (backward)
+  float* col_slab;               // per-workgroup partials
+  const void* score;             // mask-conv output rows [M*Kp][C*N] (pre-nonlinearity)
+  float* frames;                 // [M][C][Kp][L]
+  float* est;                    // [M][C][T]
+  const float* gest;             // dL/dest [M][C][T]
+  void* gscore;                  // dL/dscore rows (backward)
+  void* gwdec_out;               // dL/dw from the decoder rows (backward)
+};
+
+hipError_t launch_enc_fwd(DType dt, const CodecArgs& a, hipStream_t s);
+hipError_t launch_enc_bwd_rows(DType dt, const CodecArgs& a, hipStream_t s);
+int frame_outer_chunks(const CodecArgs& a);
+hipError_t launch_frame_outer(DType dt, int mode, const CodecArgs& a, hipStream_t s);
+hipError_t launch_dec_fwd(DType dt, const CodecArgs& a, hipStream_t s);
+hipError_t launch_dec_bwd(DType dt, const CodecArgs& a, hipStream_t s);
+
+// ---- PIT SI-SNR (pit_criterion.py) ----------------------------------------
+struct PitArgs {
+  int M, C, T;
+  const float* src;              // [M][C][T]
+  const float* est;              // [M][C][T]
+  const int64_t* lengths;        // [M]
+  double* slab;                  // [M][chunks][NV]
+  int chunks;
+  float* max_snr;                // [M]
+  int64_t* best;                 // [M] argmax permutation index
+  float* coef;                   // [M][C][4]: alpha, beta, offset, target index
+  float* loss;                   // [1]
+  const float* g_loss;           // upstream dL/d loss [1] (backward)
+  const float* g_maxsnr;         // upstream dL/d max_snr [M] or null (backward)
+  float* gest;                   // [M][C][T] (backward)
+  float* est_inplace;            // est to mask in place (forward)
+  float* reordered;              // [M][C][T]
+  int nperm;
+  int perms[24][4];              // lexicographic permutations of range(C)
+};
+int pit_nv(int C);
+hipError_t launch_pit_forward(const PitArgs& a, hipStream_t s);
+hipError_t launch_pit_backward(const PitArgs& a, hipStream_t s);
+
+}  // namespace ctn

@@ -1,0 +1,468 @@
+// Encoder / decoder / overlap-add kernels (gfx950).
+//
+// enc_fwd     : w[r][n] = ReLU(sum_l U[n][l] x[m, k*S + l])          conv_tasnet.py:106,116
+//               + per-frame cLN statistics of w (two-pass, fp32)     conv_tasnet.py:167,319-329
+// enc_bwd_rows: cLN backward per frame, + decoder's dL/dw, ReLU mask -> dL/d(pre-ReLU)
+// frame_outer : dU[n][l] = sum_r g[r][n] x[kS+l]  (encoder weight grad) and
+//               dV[l][n] = sum_{r,c} src_c[r][n] gest_c[kS+l] (decoder basis grad)
+// dec_fwd     : frames[m][c][k][l] = sum_n (w[r][n] * act(score)[r][c][n]) V[l][n]   :128-140
+// ola_fwd     : est[m][c][t] = sum_{k: kS<=t<kS+L} frames[m][c][k][t-kS], zero to T  utils.py:9-46, :56-59
+// dec_bwd     : dL/dscore and dL/dw from dL/dest (frames gradient gathered from est)
+#include "ctn_common.h"
+#include "ctn_codec.h"
+
+namespace ctn {
+
+constexpr int EN_RPB = 128;   // frame rows per workgroup (matches the row padding)
+
+// ===========================================================================
+// encoder forward
+// ===========================================================================
+template <typename T>
+__global__ __launch_bounds__(256) void enc_fwd_kernel(CodecArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int N = a.N, L = a.L, S = a.S, cg = N / 8;
+  int nrl = 256 / cg;
+  if (nrl > EN_RPB) nrl = EN_RPB;
+  const int tid = threadIdx.x, c = tid % cg, rl = tid / cg;
+  const bool act = rl < nrl;
+  const int K = a.K, Kp = a.Kp;
+  const int row0 = blockIdx.x * EN_RPB, m = row0 / Kp, k0 = row0 - m * Kp;
+  float* Ut = sm;                           // [L][N]
+  float* xs = sm + L * N;                   // samples [k0*S, k0*S + (EN_RPB-1)*S + L)
+  const int nsamp = (EN_RPB - 1) * S + L;
+  for (int i = tid; i < L * N; i += 256) {
+    const int l = i / N, n = i % N;
+    Ut[i] = a.U[n * L + l];
+  }
+  for (int i = tid; i < nsamp; i += 256) {
+    const long t = (long)k0 * S + i;
+    xs[i] = t < a.T ? a.mixture[(size_t)m * a.T + t] : 0.f;
+  }
+  __syncthreads();
+  T* w = reinterpret_cast<T*>(a.w_rows);
+  if (!act) return;
+  for (int rr = rl; rr < EN_RPB; rr += nrl) {
+    const int k = k0 + rr;
+    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (k < K) {
+      for (int l = 0; l < L; ++l) {
+        const float x = xs[rr * S + l];
+        const float4 u0 = *reinterpret_cast<const float4*>(Ut + l * N + c * 8);
+        const float4 u1 = *reinterpret_cast<const float4*>(Ut + l * N + c * 8 + 4);
+        v[0] += u0.x * x; v[1] += u0.y * x; v[2] += u0.z * x; v[3] += u0.w * x;
+        v[4] += u1.x * x; v[5] += u1.y * x; v[6] += u1.z * x; v[7] += u1.w * x;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+    }
+    Vec8<T>::store(w + (size_t)(row0 + rr) * N + c * 8, v);
+    if (a.cln_stats) {
+      // two-pass per-frame statistics over the N channels (cg lanes of one wave)
+      float s = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += v[e];
+      s = wave_sum_group(s, cg);
+      const float mean = s / (float)N;
+      float q = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) q += (v[e] - mean) * (v[e] - mean);
+      q = wave_sum_group(q, cg);
+      if (c == 0) {
+        const float rstd = 1.0f / sqrtf(q / (float)N + 1e-8f);
+        a.cln_stats[row0 + rr] = k < K ? make_float2(mean, rstd) : make_float2(0.f, 1.f);
+      }
+    }
+  }
+}
+
+// ===========================================================================
+// encoder backward (rows): cLN backward + decoder grad + ReLU mask
+//   gcln : dL/d cLN(w)  [rows][N] storage type (bottleneck data gradient)
+//   gwdec: dL/dw from the decoder [rows][N] storage type (may be null)
+//   out  : gpre [rows][N] fp32 = dL/d(pre-ReLU encoder output)
+//   col partials per block: ggamma0[N], gbeta0[N]
+// ===========================================================================
+template <typename T>
+__global__ __launch_bounds__(256) void enc_bwd_rows_kernel(CodecArgs a) {
+  __shared__ float buf[256 * 8];
+  const int N = a.N, cg = N / 8;
+  int nrl = 256 / cg;
+  if (nrl > EN_RPB) nrl = EN_RPB;
+  const int tid = threadIdx.x, c = tid % cg, rl = tid / cg;
+  const bool act = rl < nrl;
+  const int K = a.K, Kp = a.Kp;
+  const int row0 = blockIdx.x * EN_RPB, m = row0 / Kp, k0 = row0 - m * Kp;
+  const T* w = reinterpret_cast<const T*>(a.w_rows);
+  const T* gcln = reinterpret_cast<const T*>(a.gcln);
+  const T* gwdec = reinterpret_cast<const T*>(a.gwdec);
+  float g0[8], cgam[8], cbet[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    g0[e] = a.gamma0 ? a.gamma0[c * 8 + e] : 0.f;
+    cgam[e] = cbet[e] = 0.f;
+  }
+  if (act) {
+    for (int rr = rl; rr < EN_RPB; rr += nrl) {
+      const int r = row0 + rr, k = k0 + rr;
+      float out[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (k < K) {   // uniform across the cg lanes of this frame
+        float wv[8], gd[8];
+        Vec8<T>::load(w + (size_t)r * N + c * 8, wv);
+        if (gwdec) Vec8<T>::load(gwdec + (size_t)r * N + c * 8, gd);
+        else
+#pragma unroll
+          for (int e = 0; e < 8; ++e) gd[e] = 0.f;
+        if (gcln) {
+          float gv[8];
+          Vec8<T>::load(gcln + (size_t)r * N + c * 8, gv);
+          const float2 st = a.cln_stats[r];
+          float s1 = 0.f, s2 = 0.f, wh[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            wh[e] = (wv[e] - st.x) * st.y;
+            const float gh = gv[e] * g0[e];
+            s1 += gh;
+            s2 += gh * wh[e];
+            cgam[e] += gv[e] * wh[e];
+            cbet[e] += gv[e];
+          }
+          s1 = wave_sum_group(s1, cg) / (float)N;
+          s2 = wave_sum_group(s2, cg) / (float)N;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) gd[e] += st.y * (gv[e] * g0[e] - s1 - wh[e] * s2);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) out[e] = wv[e] > 0.f ? gd[e] : 0.f;   // ReLU backward
+      }
+      Vec8<float>::store(a.gpre + (size_t)r * N + c * 8, out);
+    }
+  }
+  if (a.col_slab) {
+    float* cs = a.col_slab + (size_t)blockIdx.x * 2 * N;
+    for (int q = 0; q < 2; ++q) {
+      if (act)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) buf[rl * N + c * 8 + e] = q == 0 ? cgam[e] : cbet[e];
+      __syncthreads();
+      for (int ch = tid; ch < N; ch += 256) {
+        float s = 0.f;
+        for (int i = 0; i < nrl; ++i) s += buf[i * N + ch];
+        cs[q * N + ch] = s;
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// ===========================================================================
+// frame_outer: out[n][l] partial over a chunk of frame rows
+//   mode 0 (encoder dU):  sum_r gpre[r][n] * x[m][kS + l]
+//   mode 1 (decoder dV):  sum_r sum_c (w[r][n] act_c(score[r][.][n])) * gest[m][c][kS + l]
+// workgroup = chunk of rows inside one utterance; thread = channel n (looped)
+// slab layout: [chunks][N][L]
+// ===========================================================================
+template <typename T, int MODE>
+__global__ __launch_bounds__(256) void frame_outer_kernel(CodecArgs a, int rows_per_chunk) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int N = a.N, L = a.L, S = a.S, C = MODE == 0 ? 1 : a.C, K = a.K, Kp = a.Kp;
+  const int chunks_per_utt = (Kp + rows_per_chunk - 1) / rows_per_chunk;
+  const int m = blockIdx.x / chunks_per_utt, ch = blockIdx.x % chunks_per_utt;
+  const int kb = ch * rows_per_chunk;
+  int ke = kb + rows_per_chunk;
+  if (ke > K) ke = K;
+  const int nk = ke > kb ? ke - kb : 0;
+  // signal samples for this chunk, per speaker: [C][nk*S + L]
+  const int span = rows_per_chunk * S + L;
+  for (int i = threadIdx.x; i < C * span; i += 256) {
+    const int cc = i / span, j = i % span;
+    const long t = (long)kb * S + j;
+    float v = 0.f;
+    if (MODE == 0) v = t < a.T ? a.mixture[(size_t)m * a.T + t] : 0.f;
+    else v = t < a.T ? a.gest[((size_t)m * a.C + cc) * a.T + t] : 0.f;
+    sm[i] = v;
+  }
+  __syncthreads();
+  const T* w = reinterpret_cast<const T*>(a.w_rows);
+  const T* sc = reinterpret_cast<const T*>(a.score);
+  float* out = a.col_slab + (size_t)blockIdx.x * N * L;
+  for (int n = threadIdx.x; n < N; n += 256) {
+    float acc[32];
+#pragma unroll
+    for (int l = 0; l < 32; ++l) acc[l] = 0.f;
+    for (int kk = 0; kk < nk; ++kk) {
+      const size_t r = (size_t)m * Kp + kb + kk;
+      if constexpr (MODE == 0) {
+        const float g = a.gpre[r * N + n];
+        const float* xs = sm + kk * S;
+#pragma unroll
+        for (int l = 0; l < 32; ++l)
+          if (l < L) acc[l] += g * xs[l];
+      } else {
+        const float wv = ld1<T>(w + r * N + n);
+        float sv[4];
+        float mx = -3.4e38f, den = 0.f;
+        for (int cc = 0; cc < C; ++cc) {
+          sv[cc] = ld1<T>(sc + r * (size_t)(C * N) + (size_t)cc * N + n);
+          mx = fmaxf(mx, sv[cc]);
+        }
+        if (a.mask_type == 1) {
+          for (int cc = 0; cc < C; ++cc) { sv[cc] = __expf(sv[cc] - mx); den += sv[cc]; }
+          for (int cc = 0; cc < C; ++cc) sv[cc] /= den;
+        } else if (a.mask_type == 0) {
+          for (int cc = 0; cc < C; ++cc) sv[cc] = sv[cc] > 0.f ? sv[cc] : 0.f;
+        }
+        for (int cc = 0; cc < C; ++cc) {
+          const float src = wv * sv[cc];
+          const float* gs = sm + cc * span + kk * S;
+#pragma unroll
+          for (int l = 0; l < 32; ++l)
+            if (l < L) acc[l] += src * gs[l];
+        }
+      }
+    }
+    // mode 0 -> [N][L] (encoder weight [N,1,L]); mode 1 -> [L][N] (Linear(N, L) weight)
+#pragma unroll
+    for (int l = 0; l < 32; ++l)
+      if (l < L) out[MODE == 0 ? (size_t)n * L + l : (size_t)l * N + n] = acc[l];
+  }
+}
+
+// ===========================================================================
+// decoder forward: frames[m][c][k][l]  (fp32)
+// workgroup = DEC_RPB frame rows; src = w * act(score) staged in LDS [rows][C][N]
+// ===========================================================================
+template <typename T>
+__global__ __launch_bounds__(256) void dec_fwd_kernel(CodecArgs a, int rpb) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int N = a.N, L = a.L, C = a.C, K = a.K, Kp = a.Kp;
+  float* Vt = sm;                       // [N][L]
+  float* src = sm + ((N * L + 3) & ~3); // [rpb][C][N]
+  const int row0 = blockIdx.x * rpb, m = row0 / Kp, k0 = row0 - m * Kp;
+  for (int i = threadIdx.x; i < N * L; i += 256) {
+    const int n = i / L, l = i % L;
+    Vt[i] = a.V[l * N + n];
+  }
+  const T* w = reinterpret_cast<const T*>(a.w_rows);
+  const T* sc = reinterpret_cast<const T*>(a.score);
+  const int cg = N / 8;
+  for (int i = threadIdx.x; i < rpb * cg; i += 256) {
+    const int rr = i / cg, c8 = i % cg;
+    const size_t r = (size_t)row0 + rr;
+    float wv[8], s[4][8];
+    Vec8<T>::load(w + r * N + c8 * 8, wv);
+    for (int cc = 0; cc < C; ++cc) Vec8<T>::load(sc + r * (size_t)(C * N) + (size_t)cc * N + c8 * 8, s[cc]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if (a.mask_type == 1) {
+        float mx = -3.4e38f, den = 0.f;
+        for (int cc = 0; cc < C; ++cc) mx = fmaxf(mx, s[cc][e]);
+        for (int cc = 0; cc < C; ++cc) { s[cc][e] = __expf(s[cc][e] - mx); den += s[cc][e]; }
+        for (int cc = 0; cc < C; ++cc) s[cc][e] /= den;
+      } else if (a.mask_type == 0) {
+        for (int cc = 0; cc < C; ++cc) s[cc][e] = s[cc][e] > 0.f ? s[cc][e] : 0.f;
+      }
+    }
+    for (int cc = 0; cc < C; ++cc)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) src[(rr * C + cc) * N + c8 * 8 + e] = wv[e] * s[cc][e];
+  }
+  __syncthreads();
+  const int nout = rpb * C * L;
+  for (int o = threadIdx.x; o < nout; o += 256) {
+    const int l = o % L, cc = (o / L) % C, rr = o / (L * C);
+    const int k = k0 + rr;
+    if (k >= K) continue;
+    const float* sp = src + (rr * C + cc) * N;
+    float acc = 0.f;
+    for (int n = 0; n < N; ++n) acc += sp[n] * Vt[n * L + l];
+    a.frames[(((size_t)m * C + cc) * Kp + k) * L + l] = acc;
+  }
+}
+
+// est[m][c][t] = sum over frames covering t; zero for t >= (K-1)S + L (F.pad, conv_tasnet.py:59)
+__global__ __launch_bounds__(256) void ola_fwd_kernel(CodecArgs a) {
+  const long total = (long)a.M * a.C * a.T;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int t = (int)(i % a.T);
+    const long mc = i / a.T;
+    const int K = a.K, S = a.S, L = a.L;
+    int khi = t / S;
+    if (khi > K - 1) khi = K - 1;
+    int klo = t - L + 1 <= 0 ? 0 : (t - L + 1 + S - 1) / S;
+    float s = 0.f;
+    const float* f = a.frames + (size_t)mc * a.Kp * L;
+    for (int k = klo; k <= khi; ++k) s += f[(size_t)k * L + (t - k * S)];
+    a.est[i] = s;
+  }
+}
+
+// ===========================================================================
+// decoder backward (rows): gsrc = gframes . V ; gw = sum_c gsrc_c act_c ; gscore
+// ===========================================================================
+template <typename T>
+__global__ __launch_bounds__(256) void dec_bwd_kernel(CodecArgs a, int rpb) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int N = a.N, L = a.L, C = a.C, S = a.S, K = a.K, Kp = a.Kp;
+  float* Vs = sm;                          // [L][N]
+  float* gf = sm + ((L * N + 3) & ~3);     // [rpb][C][L]
+  const int row0 = blockIdx.x * rpb, m = row0 / Kp, k0 = row0 - m * Kp;
+  for (int i = threadIdx.x; i < L * N; i += 256) Vs[i] = a.V[i];
+  for (int i = threadIdx.x; i < rpb * C * L; i += 256) {
+    const int l = i % L, cc = (i / L) % C, rr = i / (L * C);
+    const int k = k0 + rr;
+    const long t = (long)k * S + l;
+    gf[i] = (k < K && t < a.T) ? a.gest[((size_t)m * C + cc) * a.T + t] : 0.f;
+  }
+  __syncthreads();
+  const T* w = reinterpret_cast<const T*>(a.w_rows);
+  const T* sc = reinterpret_cast<const T*>(a.score);
+  T* gsc = reinterpret_cast<T*>(a.gscore);
+  T* gw = reinterpret_cast<T*>(a.gwdec_out);
+  const int cg = N / 8;
+  for (int i = threadIdx.x; i < rpb * cg; i += 256) {
+    const int rr = i / cg, c8 = i % cg;
+    const size_t r = (size_t)row0 + rr;
+    const int k = k0 + rr;
+    float gwv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (k >= K) {
+      for (int cc = 0; cc < C; ++cc) Vec8<T>::store(gsc + r * (size_t)(C * N) + (size_t)cc * N + c8 * 8, gwv);
+      Vec8<T>::store(gw + r * N + c8 * 8, gwv);
+      continue;
+    }
+    float wv[8], s[4][8], ga[4][8];
+    Vec8<T>::load(w + r * N + c8 * 8, wv);
+    for (int cc = 0; cc < C; ++cc) Vec8<T>::load(sc + r * (size_t)(C * N) + (size_t)cc * N + c8 * 8, s[cc]);
+    // gsrc[cc][e] = sum_l gf[rr][cc][l] * V[l][n]
+    for (int cc = 0; cc < C; ++cc) {
+      float g[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      const float* gfp = gf + (rr * C + cc) * L;
+      for (int l = 0; l < L; ++l) {
+        const float gl = gfp[l];
+        const float4 v0 = *reinterpret_cast<const float4*>(Vs + l * N + c8 * 8);
+        const float4 v1 = *reinterpret_cast<const float4*>(Vs + l * N + c8 * 8 + 4);
+        g[0] += gl * v0.x; g[1] += gl * v0.y; g[2] += gl * v0.z; g[3] += gl * v0.w;
+        g[4] += gl * v1.x; g[5] += gl * v1.y; g[6] += gl * v1.z; g[7] += gl * v1.w;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ga[cc][e] = g[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float act[4];
+      if (a.mask_type == 1) {
+        float mx = -3.4e38f, den = 0.f;
+        for (int cc = 0; cc < C; ++cc) mx = fmaxf(mx, s[cc][e]);
+        for (int cc = 0; cc < C; ++cc) { act[cc] = __expf(s[cc][e] - mx); den += act[cc]; }
+        for (int cc = 0; cc < C; ++cc) act[cc] /= den;
+      } else if (a.mask_type == 0) {
+        for (int cc = 0; cc < C; ++cc) act[cc] = s[cc][e] > 0.f ? s[cc][e] : 0.f;
+      } else {
+        for (int cc = 0; cc < C; ++cc) act[cc] = s[cc][e];
+      }
+      float gw_e = 0.f, dot = 0.f;
+      for (int cc = 0; cc < C; ++cc) {
+        gw_e += ga[cc][e] * act[cc];
+        ga[cc][e] *= wv[e];                 // dL/d act_c
+        dot += ga[cc][e] * act[cc];
+      }
+      gwv[e] = gw_e;
+      for (int cc = 0; cc < C; ++cc) {
+        float g;
+        if (a.mask_type == 1) g = act[cc] * (ga[cc][e] - dot);
+        else if (a.mask_type == 0) g = s[cc][e] > 0.f ? ga[cc][e] : 0.f;
+        else g = ga[cc][e];
+        s[cc][e] = g;
+      }
+    }
+    for (int cc = 0; cc < C; ++cc) Vec8<T>::store(gsc + r * (size_t)(C * N) + (size_t)cc * N + c8 * 8, s[cc]);
+    Vec8<T>::store(gw + r * N + c8 * 8, gwv);
+  }
+}
+
+// ===========================================================================
+// launchers
+// ===========================================================================
+static bool codec_ok(const CodecArgs& a) {
+  return a.N % 8 == 0 && a.N / 8 <= 64 && ((a.N / 8) & (a.N / 8 - 1)) == 0 && a.L >= 1 && a.L <= 32 &&
+         a.S >= 1 && a.C >= 1 && a.C <= 4 && a.Kp % EN_RPB == 0;
+}
+
+hipError_t launch_enc_fwd(DType dt, const CodecArgs& a, hipStream_t s) {
+  if (!codec_ok(a)) return hipErrorInvalidValue;
+  const size_t lds = ((size_t)a.L * a.N + (EN_RPB - 1) * a.S + a.L) * sizeof(float);
+  const dim3 g((unsigned)((long)a.M * a.Kp / EN_RPB)), b(256);
+  if (dt == BF16) hipLaunchKernelGGL(enc_fwd_kernel<bf16raw>, g, b, lds, s, a);
+  else hipLaunchKernelGGL(enc_fwd_kernel<float>, g, b, lds, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_enc_bwd_rows(DType dt, const CodecArgs& a, hipStream_t s) {
+  if (!codec_ok(a)) return hipErrorInvalidValue;
+  const dim3 g((unsigned)((long)a.M * a.Kp / EN_RPB)), b(256);
+  if (dt == BF16) hipLaunchKernelGGL(enc_bwd_rows_kernel<bf16raw>, g, b, 0, s, a);
+  else hipLaunchKernelGGL(enc_bwd_rows_kernel<float>, g, b, 0, s, a);
+  return hipGetLastError();
+}
+
+int frame_outer_rows_per_chunk(const CodecArgs& a) {
+  // 256 frames per workgroup: M * Kp / 256 workgroups (400 at the paper batch)
+  const int r = 256;
+  return r < a.Kp ? r : a.Kp;
+}
+int frame_outer_chunks(const CodecArgs& a) {
+  const int rpc = frame_outer_rows_per_chunk(a);
+  return a.M * ((a.Kp + rpc - 1) / rpc);
+}
+
+hipError_t launch_frame_outer(DType dt, int mode, const CodecArgs& a, hipStream_t s) {
+  if (!codec_ok(a)) return hipErrorInvalidValue;
+  const int rpc = frame_outer_rows_per_chunk(a);
+  const int C = mode == 0 ? 1 : a.C;
+  const size_t lds = (size_t)C * (rpc * a.S + a.L) * sizeof(float);
+  const dim3 g(frame_outer_chunks(a)), b(256);
+  if (mode == 0) {
+    if (dt == BF16) hipLaunchKernelGGL((frame_outer_kernel<bf16raw, 0>), g, b, lds, s, a, rpc);
+    else hipLaunchKernelGGL((frame_outer_kernel<float, 0>), g, b, lds, s, a, rpc);
+  } else {
+    if (dt == BF16) hipLaunchKernelGGL((frame_outer_kernel<bf16raw, 1>), g, b, lds, s, a, rpc);
+    else hipLaunchKernelGGL((frame_outer_kernel<float, 1>), g, b, lds, s, a, rpc);
+  }
+  return hipGetLastError();
+}
+
+static int dec_rpb(const CodecArgs& a) {
+  // 64 KB of LDS: the [N][L] basis plus rpb frame rows of src; rpb divides 128
+  const size_t budget = 64 * 1024 - (((size_t)a.N * a.L + 3) & ~(size_t)3) * 4;
+  int rpb = 32;
+  while (rpb > 1 && (size_t)rpb * a.C * a.N * 4 > budget) rpb >>= 1;
+  return rpb;
+}
+
+hipError_t launch_dec_fwd(DType dt, const CodecArgs& a, hipStream_t s) {
+  if (!codec_ok(a)) return hipErrorInvalidValue;
+  const int rpb = dec_rpb(a);
+  const size_t lds = (((size_t)a.N * a.L + 3) & ~(size_t)3) * 4 + (size_t)rpb * a.C * a.N * 4;
+  const dim3 g((unsigned)((long)a.M * a.Kp / rpb)), b(256);
+  if (dt == BF16) hipLaunchKernelGGL(dec_fwd_kernel<bf16raw>, g, b, lds, s, a, rpb);
+  else hipLaunchKernelGGL(dec_fwd_kernel<float>, g, b, lds, s, a, rpb);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  long total = (long)a.M * a.C * a.T;
+  int gb = (int)((total + 255) / 256);
+  if (gb > 4096) gb = 4096;
+  hipLaunchKernelGGL(ola_fwd_kernel, dim3(gb), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_dec_bwd(DType dt, const CodecArgs& a, hipStream_t s) {
+  if (!codec_ok(a)) return hipErrorInvalidValue;
+  const int rpb = 32;
+  const size_t lds = (((size_t)a.N * a.L + 3) & ~(size_t)3) * 4 + (size_t)rpb * a.C * a.L * 4;
+  const dim3 g((unsigned)((long)a.M * a.Kp / rpb)), b(256);
+  if (dt == BF16) hipLaunchKernelGGL(dec_bwd_kernel<bf16raw>, g, b, lds, s, a, rpb);
+  else hipLaunchKernelGGL(dec_bwd_kernel<float>, g, b, lds, s, a, rpb);
+  return hipGetLastError();
+}
+
+}  // namespace ctn

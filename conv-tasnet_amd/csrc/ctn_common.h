@@ -59,6 +59,28 @@ template <> struct Vec8<bf16raw> {
   }
 };
 
+// Raw 8-element vector: loaded as-is (bf16: 4 dwords, f32: 8 dwords) so many
+// loads can be in flight in few registers; unpacked to fp32 at the point of use.
+template <typename T> struct Raw8;
+template <> struct Raw8<bf16raw> {
+  u128 v;
+  CTN_DEV void load(const bf16raw* p) { v = *reinterpret_cast<const u128*>(p); }
+  CTN_DEV float operator[](int e) const {
+    const uint32_t w = e < 2 ? v.x : e < 4 ? v.y : e < 6 ? v.z : v.w;
+    return (e & 1) ? __uint_as_float(w & 0xffff0000u) : __uint_as_float(w << 16);
+  }
+};
+template <> struct Raw8<float> {
+  float4 a, b;
+  CTN_DEV void load(const float* p) {
+    a = *reinterpret_cast<const float4*>(p);
+    b = *reinterpret_cast<const float4*>(p + 4);
+  }
+  CTN_DEV float operator[](int e) const {
+    return e == 0 ? a.x : e == 1 ? a.y : e == 2 ? a.z : e == 3 ? a.w : e == 4 ? b.x : e == 5 ? b.y : e == 6 ? b.z : b.w;
+  }
+};
+
 // 4-element store (GEMM epilogue: one lane owns 4 consecutive output columns)
 template <typename T> CTN_DEV void store4(T* p, const float v[4]);
 template <> CTN_DEV void store4<float>(float* p, const float v[4]) {

@@ -51,6 +51,17 @@ class TBlockSaved(ctypes.Structure):
     _fields_ = [("h1", c_void_p), ("d", c_void_p), ("stats", c_void_p)]
 
 
+class CodecDesc(ctypes.Structure):
+    _fields_ = [(n, c_int32) for n in ("M", "T", "K", "Kp", "N", "L", "B", "C", "mask_type", "dtype")]
+
+
+class PitDesc(ctypes.Structure):
+    _fields_ = [(n, c_int32) for n in ("M", "C", "T")]
+
+
+MASK_IDENTITY = 2
+
+
 # ----------------------------------------------------------------------------
 _lib = None
 _lock = threading.Lock()
@@ -65,6 +76,15 @@ _SIGS = {
                                           c_void_p, c_size_t, c_void_p]),
     "ctn_tblock_backward": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                            c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "ctn_encoder_workspace_bytes": (c_size_t, [c_void_p, ctypes.c_int]),
+    "ctn_encoder_forward": (ctypes.c_int, [c_void_p] + [c_void_p] * 8 + [c_void_p, c_size_t, c_void_p]),
+    "ctn_encoder_backward": (ctypes.c_int, [c_void_p] + [c_void_p] * 13 + [c_void_p, c_size_t, c_void_p]),
+    "ctn_decoder_workspace_bytes": (c_size_t, [c_void_p, ctypes.c_int]),
+    "ctn_decoder_forward": (ctypes.c_int, [c_void_p] + [c_void_p] * 6 + [c_void_p, c_size_t, c_void_p]),
+    "ctn_decoder_backward": (ctypes.c_int, [c_void_p] + [c_void_p] * 10 + [c_void_p, c_size_t, c_void_p]),
+    "ctn_pit_workspace_bytes": (c_size_t, [c_void_p]),
+    "ctn_pit_forward": (ctypes.c_int, [c_void_p] + [c_void_p] * 8 + [c_void_p, c_size_t, c_void_p]),
+    "ctn_pit_backward": (ctypes.c_int, [c_void_p] + [c_void_p] * 7 + [c_void_p]),
     "ctn_timer_enable": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "ctn_timer_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
 }

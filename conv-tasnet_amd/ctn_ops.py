@@ -98,3 +98,167 @@ def rows_to_ncw(r: torch.Tensor, fr: Frames, dtype=None) -> torch.Tensor:
     C = r.shape[1]
     t = r.view(fr.M, fr.Kp, C)[:, :fr.K].transpose(1, 2)
     return t.to(dtype) if dtype is not None else t
+
+
+# ----------------------------------------------------------------------------
+# front: Encoder (conv_tasnet.py:97-117) + separator cLN (:167) + bottleneck (:169)
+# ----------------------------------------------------------------------------
+def codec_desc(fr: Frames, T, N, Lf, B, C, mask_type, dtype):
+    return L.CodecDesc(fr.M, T, fr.K, fr.Kp, N, Lf, B, C, mask_type, L.dtype_code(dtype))
+
+
+class EncoderFn(torch.autograd.Function):
+    """mixture [M,T] fp32 -> (w_rows [M*Kp,N], x0 [M*Kp,B] or None).  Wb None: encoder only."""
+
+    @staticmethod
+    def forward(ctx, mixture, fr: Frames, geo: tuple, act_dtype, U, gamma0, beta0, Wb):
+        N, Lf, B, C = geo
+        lib = L.load()
+        L.require_device(mixture, "Encoder")
+        mixture = _f32(mixture)
+        T = mixture.shape[-1]
+        U = _f32(U)
+        has_b = Wb is not None
+        g0, b0, wb = (_f32(gamma0), _f32(beta0), _f32(Wb)) if has_b else (None, None, None)
+        desc = codec_desc(fr, T, N, Lf, B if has_b else 8, C, L.MASK_RELU, act_dtype)
+        dev = mixture.device
+        w_rows = torch.empty(fr.rows, N, dtype=act_dtype, device=dev)
+        stats = torch.empty(fr.rows, 2, dtype=torch.float32, device=dev) if has_b else None
+        x0 = torch.empty(fr.rows, B, dtype=act_dtype, device=dev) if has_b else None
+        nb = lib.ctn_encoder_workspace_bytes(ctypes.byref(desc), 0)
+        ws = L.workspace(nb, dev)
+        L.check(lib.ctn_encoder_forward(ctypes.byref(desc), mixture.data_ptr(), U.data_ptr(), L.ptr(g0), L.ptr(b0),
+                                        L.ptr(wb), w_rows.data_ptr(), L.ptr(stats), L.ptr(x0), ws.data_ptr(), nb,
+                                        L.stream_handle(dev)), "ctn_encoder_forward")
+        ctx.desc = tuple(getattr(desc, f) for f, _ in L.CodecDesc._fields_)
+        ctx.has_b = has_b
+        ctx.save_for_backward(mixture, U, g0, b0, wb, w_rows, stats)
+        if not has_b:
+            return w_rows, w_rows.new_empty(0)
+        return w_rows, x0
+
+    @staticmethod
+    def backward(ctx, g_w, g_x0):
+        lib = L.load()
+        mixture, U, g0, b0, wb, w_rows, stats = ctx.saved_tensors
+        desc = L.CodecDesc(*ctx.desc)
+        dev = mixture.device
+        if g_w is not None:
+            g_w = g_w.to(w_rows.dtype).contiguous()
+        if not ctx.has_b or g_x0 is None or g_x0.numel() == 0:
+            g_x0 = None
+        else:
+            g_x0 = g_x0.to(w_rows.dtype).contiguous()
+        gU = torch.empty_like(U)
+        gg0 = torch.empty_like(g0) if g_x0 is not None else None
+        gb0 = torch.empty_like(b0) if g_x0 is not None else None
+        gwb = torch.empty_like(wb) if g_x0 is not None else None
+        nb = lib.ctn_encoder_workspace_bytes(ctypes.byref(desc), 1)
+        ws = L.workspace(nb, dev)
+        L.check(lib.ctn_encoder_backward(ctypes.byref(desc), mixture.data_ptr(), U.data_ptr(), L.ptr(g0),
+                                         L.ptr(b0), L.ptr(wb), w_rows.data_ptr(), L.ptr(stats), L.ptr(g_w),
+                                         L.ptr(g_x0), gU.data_ptr(), L.ptr(gg0), L.ptr(gb0), L.ptr(gwb),
+                                         ws.data_ptr(), nb, L.stream_handle(dev)), "ctn_encoder_backward")
+        if ctx.has_b and g_x0 is None:        # bottleneck output unused: zero grads
+            gg0, gb0, gwb = torch.zeros_like(g0), torch.zeros_like(b0), torch.zeros_like(wb)
+        return None, None, None, None, gU, gg0, gb0, gwb
+
+
+# ----------------------------------------------------------------------------
+# back: mask conv (:185) + nonlinearity (:202-208) + Decoder (:120-142) + OLA + pad
+# ----------------------------------------------------------------------------
+class DecoderFn(torch.autograd.Function):
+    """(x_last [M*Kp,B], w_rows [M*Kp,N]) -> est [M,C,T] fp32.
+    Wm None: standalone Decoder; x_last then holds mask rows [M*Kp, C*N]."""
+
+    @staticmethod
+    def forward(ctx, x_last, w_rows, fr: Frames, geo: tuple, Wm, V):
+        T, N, Lf, B, C, mask_type = geo
+        lib = L.load()
+        L.require_device(x_last, "Decoder")
+        x_last, w_rows = x_last.contiguous(), w_rows.contiguous()
+        V = _f32(V)
+        wm = _f32(Wm) if Wm is not None else None
+        desc = codec_desc(fr, T, N, Lf, B, C, mask_type, w_rows.dtype)
+        dev = w_rows.device
+        score = torch.empty(fr.rows, C * N, dtype=w_rows.dtype, device=dev) if wm is not None else None
+        est = torch.empty(fr.M, C, T, dtype=torch.float32, device=dev)
+        nb = lib.ctn_decoder_workspace_bytes(ctypes.byref(desc), 0)
+        ws = L.workspace(nb, dev)
+        L.check(lib.ctn_decoder_forward(ctypes.byref(desc), x_last.data_ptr(), w_rows.data_ptr(), L.ptr(wm),
+                                        V.data_ptr(), L.ptr(score), est.data_ptr(), ws.data_ptr(), nb,
+                                        L.stream_handle(dev)), "ctn_decoder_forward")
+        ctx.desc = tuple(getattr(desc, f) for f, _ in L.CodecDesc._fields_)
+        ctx.save_for_backward(x_last, w_rows, wm, V, score)
+        return est
+
+    @staticmethod
+    def backward(ctx, g_est):
+        lib = L.load()
+        x_last, w_rows, wm, V, score = ctx.saved_tensors
+        desc = L.CodecDesc(*ctx.desc)
+        dev = w_rows.device
+        g_est = _f32(g_est)
+        g_x = torch.empty_like(x_last)
+        g_w = torch.empty_like(w_rows)
+        gwm = torch.empty_like(wm) if wm is not None else None
+        gV = torch.empty_like(V)
+        nb = lib.ctn_decoder_workspace_bytes(ctypes.byref(desc), 1)
+        ws = L.workspace(nb, dev)
+        L.check(lib.ctn_decoder_backward(ctypes.byref(desc), x_last.data_ptr(), w_rows.data_ptr(), L.ptr(wm),
+                                         V.data_ptr(), L.ptr(score), g_est.data_ptr(), g_x.data_ptr(),
+                                         g_w.data_ptr(), L.ptr(gwm), gV.data_ptr(), ws.data_ptr(), nb,
+                                         L.stream_handle(dev)), "ctn_decoder_backward")
+        return g_x, g_w, None, None, gwm, gV
+
+
+# ----------------------------------------------------------------------------
+# PIT SI-SNR loss (pit_criterion.py:12-113)
+# ----------------------------------------------------------------------------
+class PITFn(torch.autograd.Function):
+    """(source, est, lengths) -> (loss, max_snr [M,1], est (masked in place), best perm idx)."""
+
+    @staticmethod
+    def forward(ctx, source, est, lengths):
+        lib = L.load()
+        L.require_device(est, "cal_loss")
+        if source.shape != est.shape:
+            raise AssertionError("source and estimate_source sizes differ")   # pit_criterion.py:34
+        if est.dtype != torch.float32 or not est.is_contiguous():
+            raise L.CtnLibraryError("estimate_source must be a contiguous float32 tensor")
+        source = _f32(source)
+        lengths = lengths.to(device=est.device, dtype=torch.int64).contiguous()
+        M, C, T = est.shape
+        desc = L.PitDesc(M, C, T)
+        dev = est.device
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        max_snr = torch.empty(M, 1, dtype=torch.float32, device=dev)
+        best = torch.empty(M, dtype=torch.int64, device=dev)
+        coef = torch.empty(M, C, 4, dtype=torch.float32, device=dev)
+        nb = lib.ctn_pit_workspace_bytes(ctypes.byref(desc))
+        ws = L.workspace(nb, dev)
+        L.check(lib.ctn_pit_forward(ctypes.byref(desc), source.data_ptr(), est.data_ptr(), lengths.data_ptr(),
+                                    loss.data_ptr(), max_snr.data_ptr(), best.data_ptr(), None, coef.data_ptr(),
+                                    ws.data_ptr(), nb, L.stream_handle(dev)), "ctn_pit_forward")
+        ctx.mark_dirty(est)
+        ctx.mark_non_differentiable(best)
+        ctx.save_for_backward(source, est, lengths, coef)
+        return loss, max_snr, est, best
+
+    @staticmethod
+    def backward(ctx, g_loss, g_max_snr, g_est_out, _g_best):
+        lib = L.load()
+        source, est, lengths, coef = ctx.saved_tensors
+        M, C, T = est.shape
+        desc = L.PitDesc(M, C, T)
+        dev = est.device
+        g_est = torch.empty_like(est)
+        gl = _f32(g_loss.reshape(1)) if g_loss is not None else torch.zeros(1, device=dev)
+        gm = _f32(g_max_snr.reshape(M)) if g_max_snr is not None else None
+        L.check(lib.ctn_pit_backward(ctypes.byref(desc), source.data_ptr(), est.data_ptr(), lengths.data_ptr(),
+                                     coef.data_ptr(), gl.data_ptr(), L.ptr(gm), g_est.data_ptr(),
+                                     L.stream_handle(dev)), "ctn_pit_backward")
+        if g_est_out is not None:
+            mask = (torch.arange(T, device=dev).unsqueeze(0) < lengths.unsqueeze(1)).unsqueeze(1)
+            g_est = g_est + g_est_out * mask
+        return None, g_est, None

@@ -96,6 +96,53 @@ int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_params* p, co
                         const ctn_tblock_grads* g, void* ws, size_t ws_bytes, void* stream);
 
 /* -------------------------------------------------------------------------
+ * Front of the network: Encoder (src/conv_tasnet.py:97-117: ReLU(Conv1d(1,N,L,
+ * stride L/2))) + the TemporalConvNet input cLN (:167, :307-329) + bottleneck
+ * 1x1 conv N->B (:169).  wb == NULL: encoder only (standalone Encoder).
+ * Back of the network: mask 1x1 conv B->C*N (:185), mask nonlinearity
+ * (:202-208), Decoder (:120-142), overlap_and_add (src/utils.py:9-46) and the
+ * F.pad to T (:56-59).  wm == NULL: standalone Decoder, `x_last` then holds
+ * the mask rows [M*Kp, C*N] and mask_type must be CTN_MASK_IDENTITY.
+ * ------------------------------------------------------------------------- */
+#define CTN_MASK_IDENTITY 2
+typedef struct {
+  int32_t M, T, K, Kp;      /* utterances, samples, frames = (T-L)/(L/2)+1, padded frames */
+  int32_t N, L, B, C;       /* encoder filters, filter length, bottleneck ch., speakers */
+  int32_t mask_type;        /* ctn_mask_type or CTN_MASK_IDENTITY */
+  int32_t dtype;            /* ctn_dtype of activations */
+} ctn_codec_desc;
+
+size_t ctn_encoder_workspace_bytes(const ctn_codec_desc* d, int backward);
+int ctn_encoder_forward(const ctn_codec_desc* d, const float* mixture, const float* U, const float* gamma0,
+                        const float* beta0, const float* wb, void* w_rows, float* cln_stats, void* x0,
+                        void* ws, size_t ws_bytes, void* stream);
+int ctn_encoder_backward(const ctn_codec_desc* d, const float* mixture, const float* U, const float* gamma0,
+                         const float* beta0, const float* wb, const void* w_rows, const float* cln_stats,
+                         const void* g_w_rows, const void* g_x0, float* gU, float* ggamma0, float* gbeta0,
+                         float* gwb, void* ws, size_t ws_bytes, void* stream);
+
+size_t ctn_decoder_workspace_bytes(const ctn_codec_desc* d, int backward);
+int ctn_decoder_forward(const ctn_codec_desc* d, const void* x_last, const void* w_rows, const float* wm,
+                        const float* V, void* score, float* est, void* ws, size_t ws_bytes, void* stream);
+int ctn_decoder_backward(const ctn_codec_desc* d, const void* x_last, const void* w_rows, const float* wm,
+                         const float* V, const void* score, const float* g_est, void* g_x_last, void* g_w_rows,
+                         float* gwm, float* gV, void* ws, size_t ws_bytes, void* stream);
+
+/* -------------------------------------------------------------------------
+ * PIT SI-SNR loss: replaces cal_loss / cal_si_snr_with_pit / reorder_source /
+ * get_mask, src/pit_criterion.py:12-113.  `est` is masked in place beyond
+ * each length (:37-38); `reordered` (nullable) keeps the reference's
+ * perm-not-inverse indexing (:91-97).  `coef` [M*C*4] is saved for backward.
+ * ------------------------------------------------------------------------- */
+typedef struct { int32_t M, C, T; } ctn_pit_desc;
+size_t ctn_pit_workspace_bytes(const ctn_pit_desc* d);
+int ctn_pit_forward(const ctn_pit_desc* d, const float* source, float* est, const int64_t* lengths, float* loss,
+                    float* max_snr, int64_t* best_perm, float* reordered, float* coef, void* ws, size_t ws_bytes,
+                    void* stream);
+int ctn_pit_backward(const ctn_pit_desc* d, const float* source, const float* est, const int64_t* lengths,
+                     const float* coef, const float* g_loss, const float* g_max_snr, float* g_est, void* stream);
+
+/* -------------------------------------------------------------------------
  * Opt-in kernel timer (bench.py roofline): when enabled, every launch of the
  * selected kernel family is bracketed by hipEvents on its stream.
  * kind: 0 off, 1 block-forward first 1x1 GEMM, 2 depthwise forward,

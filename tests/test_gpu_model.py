@@ -1,0 +1,175 @@
+"""Full-model, encoder/decoder and PIT-loss HIP paths vs the reference's golden
+vectors (tests/golden, captured from jwr1995/Conv-TasNet) and the CPU oracle.
+GPU only.  Tolerances: fp32 mode — 1e-4 relative on outputs, 2e-3 on
+gradients (fp32 MFMA, different reduction order); bf16 mode — SI-SNRi within
+0.1 dB of the reference (BASELINE.json north_star) and 5e-2 relative L2 on
+the estimate."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import ctn_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def load(name):
+    return np.load(os.path.join(GOLDEN, name))
+
+
+def T(a, dev=DEV):
+    return torch.from_numpy(np.array(a)).to(dev)
+
+
+def rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
+
+
+def cfg_of(g):
+    N, L, B, H, P, X, R, C = [int(v) for v in g["cfg"]]
+    return O.Cfg(N, L, B, H, P, X, R, C, str(g["cfg_norm"]), bool(int(g["cfg_causal"])), str(g["cfg_mask"]))
+
+
+def build(cfg, g):
+    import conv_tasnet as ct
+    m = ct.ConvTasNet(cfg.N, cfg.L, cfg.B, cfg.H, cfg.P, cfg.X, cfg.R, cfg.C, norm_type=cfg.norm_type,
+                      causal=cfg.causal, mask_nonlinear=cfg.mask_nonlinear)
+    if "p:encoder.conv1d_U.weight" in g.files:
+        sd = {n: torch.from_numpy(g["p:" + n]) for n, _ in O.param_shapes(cfg)}
+    else:
+        sd = O.init_params(cfg, int(g["seed"]))
+    m.load_state_dict(sd, strict=False)
+    return m.to(DEV)
+
+
+def run(model, g, bf16=False):
+    import pit_criterion as pc
+    mix, src, lens = T(g["mix"]), T(g["src"]), T(g["len"])
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=bf16):
+        est = model(mix)
+    loss, max_snr, est_m, reord = pc.cal_loss(src, est, lens)
+    model.zero_grad()
+    loss.backward()
+    return est_m, loss, max_snr, reord
+
+
+MODELS = ["model_c1.npz", "model_paper_short.npz", "model_causal_cln.npz", "model_3spk.npz",
+          "model_softmax_pad.npz"]
+
+
+@pytest.mark.parametrize("name", MODELS)
+def test_model_fp32_vs_reference(name):
+    g = load(name)
+    cfg = cfg_of(g)
+    model = build(cfg, g)
+    est, loss, max_snr, reord = run(model, g)
+    scale = float(np.abs(g["est"]).max())
+    np.testing.assert_allclose(est.detach().cpu().numpy(), g["est"], rtol=1e-3, atol=2e-4 * scale)
+    assert rel(est.detach().cpu().numpy(), g["est"]) < 1e-4
+    np.testing.assert_allclose(float(loss), float(g["loss"]), rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(max_snr.detach().cpu().numpy(), g["max_snr"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(reord.cpu().numpy(), g["reord"], rtol=1e-3, atol=2e-4 * scale)
+    params = dict(model.named_parameters())
+    for n, shape in O.param_shapes(cfg):
+        gr = params[n].grad.detach().cpu().reshape(-1).numpy()
+        gn = float(g["gnorm:" + n])
+        if shape == (1,):
+            # PReLU alpha: one sum over M*K*H terms with heavy cancellation; the fp32
+            # reduction order alone moves it by ~1e-4 absolute
+            np.testing.assert_allclose(gr, g["ghead:" + n], rtol=2e-3, atol=1e-3, err_msg=n)
+            continue
+        np.testing.assert_allclose(np.linalg.norm(gr), gn, rtol=2e-3, atol=1e-6, err_msg=n)
+        np.testing.assert_allclose(gr[:64], g["ghead:" + n], rtol=2e-3, atol=2e-3 * gn + 1e-7, err_msg=n)
+        if "g:" + n in g.files:
+            assert rel(gr, g["g:" + n].reshape(-1)) < 2e-3, n
+    if cfg.C == 2:
+        for b in range(est.shape[0]):
+            l = int(g["len"][b])
+            v = O.cal_sisnri(g["src"][b, :, :l], reord[b, :, :l].cpu().numpy(), g["mix"][b, :l])
+            assert abs(v - g["sisnri"][b]) < 1e-3
+
+
+@pytest.mark.parametrize("name", ["model_paper_short.npz", "model_c1.npz", "model_causal_cln.npz"])
+def test_model_bf16_sisnri_within_0p1db(name):
+    g = load(name)
+    cfg = cfg_of(g)
+    model = build(cfg, g)
+    est, loss, max_snr, reord = run(model, g, bf16=True)
+    assert rel(est.detach().cpu().numpy(), g["est"]) < 5e-2
+    assert abs(float(loss) - float(g["loss"])) < 0.1
+    for b in range(est.shape[0]):
+        l = int(g["len"][b])
+        v = O.cal_sisnri(g["src"][b, :, :l], reord[b, :, :l].cpu().numpy(), g["mix"][b, :l])
+        assert abs(v - g["sisnri"][b]) < 0.1, (v, g["sisnri"][b])
+    # bf16-mode weight gradients: measured 2-5 % relative L2 error vs fp32 on the paper
+    # dims (bf16 activations through 32 residual blocks); checked as norm agreement, and
+    # as full-tensor relative error where the fixture holds the full gradient
+    params = dict(model.named_parameters())
+    for n, shape in O.param_shapes(cfg):
+        if len(shape) < 2:
+            continue
+        gr = params[n].grad.detach().cpu().reshape(-1).numpy()
+        assert abs(np.linalg.norm(gr) / float(g["gnorm:" + n]) - 1) < 0.1, n
+        if "g:" + n in g.files:
+            assert rel(gr, g["g:" + n].reshape(-1)) < 0.1, n
+
+
+def test_bn_is_reported_unsupported():
+    import ctn_lib as L
+    g = load("model_bn.npz")
+    cfg = cfg_of(g)
+    model = build(cfg, g)
+    with pytest.raises(L.CtnLibraryError):
+        model(T(g["mix"]))
+
+
+@pytest.mark.parametrize("L_", [20, 16])
+def test_encoder_standalone(L_):
+    import conv_tasnet as ct
+    g = load("ops.npz")
+    enc = ct.Encoder(L_, 32).to(DEV)
+    enc.conv1d_U.weight.data.copy_(T(g[f"enc{L_}.U"]))
+    out = enc(T(g[f"enc{L_}.x"]))
+    (out * T(g[f"enc{L_}.G"])).sum().backward()
+    np.testing.assert_allclose(out.detach().cpu().numpy(), g[f"enc{L_}.out"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(enc.conv1d_U.weight.grad.cpu().numpy(), g[f"enc{L_}.gU"], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("L_", [20, 16])
+def test_decoder_standalone(L_):
+    import conv_tasnet as ct
+    g = load("ops.npz")
+    dec = ct.Decoder(32, L_).to(DEV)
+    dec.basis_signals.weight.data.copy_(T(g[f"dec{L_}.V"]))
+    w = T(g[f"dec{L_}.w"]).requires_grad_(True)
+    m = T(g[f"dec{L_}.m"]).requires_grad_(True)
+    out = dec(w, m)
+    (out * T(g[f"dec{L_}.G"])).sum().backward()
+    np.testing.assert_allclose(out.detach().cpu().numpy(), g[f"dec{L_}.out"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(w.grad.cpu().numpy(), g[f"dec{L_}.gw"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(m.grad.cpu().numpy(), g[f"dec{L_}.gm"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(dec.basis_signals.weight.grad.cpu().numpy(), g[f"dec{L_}.gV"], rtol=1e-4,
+                               atol=1e-3)
+
+
+@pytest.mark.parametrize("C", [2, 3])
+@pytest.mark.parametrize("tag", ["eq", "neq"])
+def test_pit_loss(C, tag):
+    import pit_criterion as pc
+    g = load("pit.npz")
+    k = f"pit.C{C}.{tag}"
+    est0 = T(g[k + ".est"]).requires_grad_(True)
+    est = est0 * 1.0
+    loss, max_snr, est_m, reord = pc.cal_loss(T(g[k + ".src"]), est, T(g[k + ".len"]))
+    assert est_m is est                                    # masked in place, same object (pit_criterion.py:24)
+    loss.backward()
+    np.testing.assert_allclose(float(loss), float(g[k + ".loss"]), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(max_snr.detach().cpu().numpy(), g[k + ".max_snr"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_array_equal(est_m.detach().cpu().numpy(), g[k + ".est_m"])
+    np.testing.assert_array_equal(reord.cpu().numpy(), g[k + ".reord"])
+    np.testing.assert_allclose(est0.grad.cpu().numpy(), g[k + ".gest"], rtol=1e-3, atol=1e-7)
