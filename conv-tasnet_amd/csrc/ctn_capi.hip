@@ -118,15 +118,14 @@ static int tb_check(const ctn_tblock_desc* d) {
                 d->K, d->Kp);
   if (d->B % 8 || d->H % 8 || d->B < 8 || d->H < 8)
     return fail(CTN_ERR_UNSUPPORTED, "B=%d H=%d must be multiples of 8", d->B, d->H);
-  if (d->H / 8 > 256) return fail(CTN_ERR_UNSUPPORTED, "H=%d > 2048", d->H);
   if (d->P < 1 || d->P > 8) return fail(CTN_ERR_UNSUPPORTED, "P=%d outside 1..8", d->P);
   if (!d->causal && d->P % 2 == 0)
     return fail(CTN_ERR_ARG, "non-causal padding (P-1)*d//2 needs odd P (conv_tasnet.py:236)");
   if (d->norm_type != CTN_NORM_GLN && d->norm_type != CTN_NORM_CLN)
     return fail(CTN_ERR_UNSUPPORTED, "norm_type %d (BN) not implemented on the HIP path", d->norm_type);
-  if (d->norm_type == CTN_NORM_CLN) {
+  {
     const int cg = d->H / 8;
-    if (cg > 64 || (cg & (cg - 1))) return fail(CTN_ERR_UNSUPPORTED, "cLN needs H/8 a power of two <= 64");
+    if (cg > 64 || (cg & (cg - 1))) return fail(CTN_ERR_UNSUPPORTED, "H=%d: need H/8 a power of two <= 64", d->H);
   }
   if (d->dtype != CTN_DTYPE_F32 && d->dtype != CTN_DTYPE_BF16) return fail(CTN_ERR_ARG, "dtype %d", d->dtype);
   if (d->dilation < 1) return fail(CTN_ERR_ARG, "dilation %d", d->dilation);
@@ -151,6 +150,10 @@ struct TbLayout {
   size_t bytes;
 };
 
+int tb_pad(const ctn_tblock_desc* d) {
+  return d->causal ? (d->P - 1) * d->dilation : (d->P - 1) * d->dilation / 2;
+}
+
 GemmRows tb_gemm1(const ctn_tblock_desc* d) {   // x[.,B] -> h1[.,H]
   GemmRows g{};
   g.g = Rows{d->M, d->K, d->Kp};
@@ -170,7 +173,7 @@ TbLayout tb_layout(const ctn_tblock_desc* d, int backward, void* ws) {
   GemmRows g1 = tb_gemm1(d);
   L.parts1 = gemm_rows_tiles_per_group(g1);
   DwArgs da{};
-  da.g = rg; da.H = d->H; da.P = d->P; da.norm = d->norm_type;
+  da.g = rg; da.H = d->H; da.P = d->P; da.norm = d->norm_type; da.dil = d->dilation; da.pad = tb_pad(d);
   L.parts2 = dw_parts_per_group(da);
   if (!backward) {
     if (d->dtype == CTN_DTYPE_BF16) {
@@ -192,7 +195,7 @@ TbLayout tb_layout(const ctn_tblock_desc* d, int backward, void* ws) {
     L.partsD = L.parts2;
     L.slabD = c.take<double2>((size_t)G * L.partsD * sizeof(double2));
     L.colD = c.take<float>((size_t)dw_blocks(da) * dw_col_stride(da) * sizeof(float));
-    L.alphaSlab = c.take<float>((size_t)dw_blocks(da) * sizeof(float));
+    L.alphaSlab = c.take<float>((size_t)ew_blocks(da) * sizeof(float));
     L.sums1 = c.take<float2>((size_t)G * sizeof(float2));
     L.sums2 = c.take<float2>((size_t)G * sizeof(float2));
     GemmCols gc{};
@@ -207,9 +210,6 @@ TbLayout tb_layout(const ctn_tblock_desc* d, int backward, void* ws) {
   return L;
 }
 
-int tb_pad(const ctn_tblock_desc* d) {
-  return d->causal ? (d->P - 1) * d->dilation : (d->P - 1) * d->dilation / 2;
-}
 }  // namespace
 
 extern "C" size_t ctn_tblock_workspace_bytes(const ctn_tblock_desc* d, int backward) {
@@ -358,7 +358,7 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
   sb.d[5] = SlabDesc{L.colD + H, gr->beta1, dwb, H, dws};
   sb.d[6] = SlabDesc{L.colD + 2 * H, gr->wd, dwb, H * d->P, dws};
   sb.d[7] = SlabDesc{L.colD + (2 + d->P) * H, gr->alpha2, dwb, 1, dws};
-  sb.d[8] = SlabDesc{L.alphaSlab, gr->alpha1, dwb, 1, 1};
+  sb.d[8] = SlabDesc{L.alphaSlab, gr->alpha1, ew_blocks(da), 1, 1};
   sb.nd = 9;
   CTN_HIP(launch_slab_reduce(sb, s));
   return CTN_OK;

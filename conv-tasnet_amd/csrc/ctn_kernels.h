@@ -106,7 +106,8 @@ struct DwArgs {
   void* gh1_out;                         // (ew) dL/dh1
   float* alpha_slab;                     // (ew) [blocks] galpha1 partials
 };
-int dw_blocks(const DwArgs& a);
+int dw_blocks(const DwArgs& a);        // depthwise (comb) kernels
+int ew_blocks(const DwArgs& a);        // norm1_bwd (128-row blocks)
 int dw_parts_per_group(const DwArgs& a);   // slab parts per utterance (gLN) or per row (cLN)
 __host__ __device__ int dw_col_stride(const DwArgs& a);
 hipError_t launch_dw_fwd(DType dt, const DwArgs& a, hipStream_t s);

@@ -18,18 +18,43 @@
 
 namespace ctn {
 
-constexpr int DW_RPB = 128;   // rows per workgroup
+constexpr int DW_RPB = 128;   // rows per workgroup (element-wise kernels)
 constexpr int DW_MAXP = 8;
+constexpr int DW_SEG = 32;    // comb steps per work item (depthwise kernels)
 
-int dw_blocks(const DwArgs& a) { return (int)(a.g.rows() / DW_RPB); }
-int dw_parts_per_group(const DwArgs& a) { return a.norm == NORM_GLN ? a.g.Kp / DW_RPB : 1; }
+// ---------------------------------------------------------------------------
+// Comb decomposition of the dilated depthwise conv.  Rows of one utterance are
+// split into residue classes rho mod d; a work item walks rows rho + j*d for
+// j in one DW_SEG-long segment.  A lane group of H/8 lanes owns one item and
+// all H channels of its rows (8 per lane, 16-byte vectors); the P taps of a
+// row are consecutive comb steps, so they live in a sliding register window:
+// every row is loaded and transformed once (plus P-1 halo rows per segment)
+// and the next row is prefetched while the current one is computed.
+// ---------------------------------------------------------------------------
+struct CombGeom {
+  int cg, ipw, jmax, nseg, items, wgpu;
+};
+__host__ __device__ inline CombGeom comb_geom(const DwArgs& a) {
+  CombGeom g;
+  g.cg = a.H / 8;
+  g.ipw = 4 * (64 / g.cg);
+  g.jmax = (a.g.Kp + a.dil - 1) / a.dil;
+  g.nseg = (g.jmax + DW_SEG - 1) / DW_SEG;
+  g.items = a.dil * g.nseg;
+  g.wgpu = (g.items + g.ipw - 1) / g.ipw;
+  return g;
+}
+
+int dw_blocks(const DwArgs& a) { return a.g.M * comb_geom(a).wgpu; }
+int dw_parts_per_group(const DwArgs& a) { return a.norm == NORM_GLN ? comb_geom(a).wgpu : 1; }
+int ew_blocks(const DwArgs& a) { return (int)(a.g.rows() / DW_RPB); }
 __host__ __device__ int dw_col_stride(const DwArgs& a) { return ((2 + a.P) * a.H + 4 + 3) & ~3; }
 
 template <int NK> CTN_DEV float2 ld_stat(const float2* s, int m, int row) {
   return NK == NORM_GLN ? s[m] : s[row];
 }
 
-// column-partial reduction: sum val[8] over row lanes, write H floats to dst.
+// column-partial reduction: sum val[8] over the lanes that own channel group c, write H floats
 CTN_DEV void col_reduce8(float* buf, const float v[8], int rl, int c, int nrl, int cg, bool act, float* dst) {
   const int H = cg * 8;
   if (act)
@@ -44,29 +69,41 @@ CTN_DEV void col_reduce8(float* buf, const float v[8], int rl, int c, int nrl, i
   __syncthreads();
 }
 
+struct CombItem {
+  int m, wgi, rho, j0, j1, base, c, sub;
+  bool active;
+};
+CTN_DEV CombItem comb_item(const DwArgs& a, const CombGeom& gm) {
+  CombItem it;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  it.c = lane % gm.cg;
+  it.sub = lane / gm.cg;
+  it.m = blockIdx.x / gm.wgpu;
+  it.wgi = blockIdx.x % gm.wgpu;
+  const int id = it.wgi * gm.ipw + wv * (64 / gm.cg) + it.sub;
+  it.active = id < gm.items;
+  it.rho = it.active ? id / gm.nseg : 0;
+  it.j0 = it.active ? (id % gm.nseg) * DW_SEG : 0;
+  it.j1 = it.j0 + DW_SEG < gm.jmax ? it.j0 + DW_SEG : gm.jmax;
+  if (!it.active) it.j1 = it.j0;
+  it.base = it.m * a.g.Kp;
+  return it;
+}
+
 // ---------------------------------------------------------------------------
-// Per-row work is written "loads first": every tap row is addressed with a
-// clamped (always valid) index, all tap loads are issued before any use, and
-// out-of-range taps are zeroed afterwards — no branch between the loads, so a
-// row costs one memory latency instead of one per tap.
+// dw_fwd: d[k] = sum_p w[p] n1[k - pad + p*dil],  n1 = norm1(PReLU(h1)) (0 outside [0,K))
 // ---------------------------------------------------------------------------
-// dw_fwd: one row = P raw tap loads (issued together) + the conv; two rows per
-// iteration keep 2P loads in flight per thread.
-// ---------------------------------------------------------------------------
-template <typename T, int NK, int P>
+template <typename T, int NK, int P, bool CAUSAL>
 __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
+  constexpr int POWN = CAUSAL ? P - 1 : (P - 1) / 2;   // tap that reads the output row itself
   __shared__ double red[16];
-  const int H = a.H, cg = H / 8;
-  int nrl = 256 / cg;
-  if (nrl > DW_RPB) nrl = DW_RPB;
-  const int tid = threadIdx.x, c = tid % cg, rl = tid / cg;
-  const bool act = rl < nrl;
-  const int K = a.g.K, Kp = a.g.Kp;
-  const int row0 = blockIdx.x * DW_RPB, m = row0 / Kp, base = m * Kp;
+  const CombGeom gm = comb_geom(a);
+  const CombItem it = comb_item(a, gm);
+  const int H = a.H, K = a.g.K, Kp = a.g.Kp, dil = a.dil, c = it.c;
   const T* h1 = reinterpret_cast<const T*>(a.h1);
   T* dout = reinterpret_cast<T*>(a.d_out);
   const float al1 = a.alpha1[0], al2 = a.alpha2[0];
-  const float2 st1u = NK == NORM_GLN ? a.st1[m] : make_float2(0.f, 0.f);
+  const float2 st1u = NK == NORM_GLN ? a.st1[it.m] : make_float2(0.f, 0.f);
 
   float w[P][8], g1[8], b1[8];
 #pragma unroll
@@ -77,101 +114,101 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
 #pragma unroll
     for (int p = 0; p < P; ++p) w[p][e] = a.wd[ch * P + p];
   }
+  // window win[i] = n1 at comb step j + (i - POWN), i in [0, P)
+  float win[P][8];
+  auto row_of = [&](int j) { return it.rho + j * dil; };
+  auto fetch = [&](int j, Raw8<T>& r, bool& ok, int& row) {
+    const int k = row_of(j);
+    ok = j >= 0 && k < K;
+    row = it.base + (ok ? k : 0);
+    r.load(h1 + (size_t)row * H + c * 8);
+  };
+  auto finish = [&](const Raw8<T>& r, bool ok, int row, float* out) {
+    const float2 st = NK == NORM_GLN ? st1u : a.st1[row];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) out[e] = ok ? (prelu(r[e], al1) - st.x) * st.y * g1[e] + b1[e] : 0.f;
+  };
+#pragma unroll
+  for (int i = 0; i < P - 1; ++i) {           // prologue: steps j0-POWN .. j0+P-2-POWN
+    Raw8<T> r; bool ok; int row;
+    fetch(it.j0 + i - POWN, r, ok, row);
+    finish(r, ok, row, win[i]);
+  }
+  Raw8<T> pre; bool pok; int prow;
+  fetch(it.j0 + P - 1 - POWN, pre, pok, prow);
   float ts = 0.f, tss = 0.f;
-  if (act) {
-    for (int rr0 = rl; rr0 < DW_RPB; rr0 += 2 * nrl) {
-      Raw8<T> v[2][P];
-      bool ok[2][P];
-      int rk[2][P];
+  for (int j = it.j0; j < it.j1; ++j) {
+    Raw8<T> cur = pre; const bool cok = pok; const int crow = prow;
+    if (j + 1 < it.j1) fetch(j + P - POWN, pre, pok, prow);
+    finish(cur, cok, crow, win[P - 1]);
+    const int k = row_of(j);
+    float out[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    float s = 0.f, ss = 0.f;
+    if (k < K) {
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int k = row0 + rr0 + u * nrl - base;
-        const int kc = k < K ? k : K - 1;
+      for (int p = 0; p < P; ++p)
 #pragma unroll
-        for (int p = 0; p < P; ++p) {
-          const int kk = k - a.pad + p * a.dil;
-          ok[u][p] = k < K && rr0 + u * nrl < DW_RPB && kk >= 0 && kk < K;
-          rk[u][p] = base + (ok[u][p] ? kk : kc);
-          v[u][p].load(h1 + (size_t)rk[u][p] * H + c * 8);
-        }
-      }
+        for (int e = 0; e < 8; ++e) out[e] += w[p][e] * win[p][e];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int rr = rr0 + u * nrl;
-        if (rr >= DW_RPB) break;
-        const int r = row0 + rr, k = r - base;
-        float out[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        float s = 0.f, ss = 0.f;
-#pragma unroll
-        for (int p = 0; p < P; ++p) {
-          const float2 st = NK == NORM_GLN ? st1u : a.st1[rk[u][p]];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float n1 = (prelu(v[u][p][e], al1) - st.x) * st.y * g1[e] + b1[e];
-            out[e] += ok[u][p] ? w[p][e] * n1 : 0.f;
-          }
-        }
-        if (k < K) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float a2 = prelu(out[e], al2);
-            s += a2;
-            ss += a2 * a2;
-          }
-        }
-        Vec8<T>::store(dout + (size_t)r * H + c * 8, out);
-        if constexpr (NK == NORM_GLN) {
-          ts += s;
-          tss += ss;
-        } else {
-          s = wave_sum_group(s, cg);
-          ss = wave_sum_group(ss, cg);
-          if (c == 0) a.slab2[r] = make_double2((double)s, (double)ss);
-        }
+      for (int e = 0; e < 8; ++e) {
+        const float a2 = prelu(out[e], al2);
+        s += a2;
+        ss += a2 * a2;
       }
     }
+    if (k < Kp) Vec8<T>::store(dout + (size_t)(it.base + k) * H + c * 8, out);
+    if constexpr (NK == NORM_GLN) {
+      ts += s;
+      tss += ss;
+    } else {
+      s = wave_sum_group(s, gm.cg);
+      ss = wave_sum_group(ss, gm.cg);
+      if (c == 0 && k < Kp) a.slab2[it.base + k] = make_double2((double)s, (double)ss);
+    }
+#pragma unroll
+    for (int i = 0; i < P - 1; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) win[i][e] = win[i + 1][e];
   }
   if constexpr (NK == NORM_GLN) {
     double v2[2] = {(double)ts, (double)tss};
     block_sum_d<2>(v2, red);
-    if (tid == 0) a.slab2[(size_t)m * (Kp / DW_RPB) + (row0 - base) / DW_RPB] = make_double2(v2[0], v2[1]);
+    if (threadIdx.x == 0) a.slab2[(size_t)it.m * gm.wgpu + it.wgi] = make_double2(v2[0], v2[1]);
   }
 }
 
 // ---------------------------------------------------------------------------
-// dw_bwd: per row 3P raw loads (d and dL/d hat a2 at the P rows whose taps read
-// this row, h1 at this row's P input taps), issued before any use.
+// dw_bwd: dL/dd (norm2 + PReLU2 backward) on a gd window, transposed depthwise
+// conv, depthwise weight gradient against an n1 window, norm1 backward sums.
+//   gd window  gdw[i] = dL/dd   at step j + (POWN - P + 1 + i)
+//   ah window  ahw[i] = hat a1  at step j + (i - POWN)
 // ---------------------------------------------------------------------------
-template <typename T, int NK, int P>
+template <typename T, int NK, int P, bool CAUSAL>
 __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
+  constexpr int POWN = CAUSAL ? P - 1 : (P - 1) / 2;
+  constexpr int GT = POWN, AT = P - 1 - POWN;           // newest step of each window, relative to j
   __shared__ double red[16];
   __shared__ float buf[256 * 8];
-  __shared__ __attribute__((aligned(16))) float sw[(P + 2) * 2048];   // [P+2][H]: taps, gamma1, beta1
-  const int H = a.H, cg = H / 8;
-  int nrl = 256 / cg;
-  if (nrl > DW_RPB) nrl = DW_RPB;
-  const int tid = threadIdx.x, c = tid % cg, rl = tid / cg;
-  const bool act = rl < nrl;
-  const int K = a.g.K, Kp = a.g.Kp;
-  const int row0 = blockIdx.x * DW_RPB, m = row0 / Kp, base = m * Kp;
+  const CombGeom gm = comb_geom(a);
+  const CombItem it = comb_item(a, gm);
+  const int H = a.H, K = a.g.K, Kp = a.g.Kp, dil = a.dil, c = it.c;
   const T* h1 = reinterpret_cast<const T*>(a.h1);
   const T* dd = reinterpret_cast<const T*>(a.d);
   const T* ga2 = reinterpret_cast<const T*>(a.ga2);
   T* ga1o = reinterpret_cast<T*>(a.ga1_out);
   const float al1 = a.alpha1[0], al2 = a.alpha2[0];
-  const int pown = a.pad / a.dil;   // the tap that reads the output row itself
   float2 st1u = make_float2(0.f, 0.f), st2u = st1u, sm2u = st1u;
-  if constexpr (NK == NORM_GLN) { st1u = a.st1[m]; st2u = a.st2[m]; sm2u = a.sm2[m]; }
+  if constexpr (NK == NORM_GLN) { st1u = a.st1[it.m]; st2u = a.st2[it.m]; sm2u = a.sm2[it.m]; }
 
-  // per-channel constants live in LDS, not in registers (this kernel is VGPR-bound)
-  for (int i = tid; i < H; i += 256) {
+  float w[P][8], g1[8], b1[8];
 #pragma unroll
-    for (int p = 0; p < P; ++p) sw[p * H + i] = a.wd[i * P + p];
-    sw[P * H + i] = a.gamma1[i];
-    sw[(P + 1) * H + i] = a.beta1[i];
+  for (int e = 0; e < 8; ++e) {
+    const int ch = c * 8 + e;
+    g1[e] = a.gamma1[ch];
+    b1[e] = a.beta1[ch];
+#pragma unroll
+    for (int p = 0; p < P; ++p) w[p][e] = a.wd[ch * P + p];
   }
-  __syncthreads();
-  auto cst = [&](int q, int e) -> float { return sw[q * H + c * 8 + e]; };
   float cgam[8], cbet[8], cwd[P][8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -181,98 +218,133 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
   }
   float calpha = 0.f, ts = 0.f, tss = 0.f;
 
-  if (act) {
-    for (int rr = rl; rr < DW_RPB; rr += nrl) {
-      const int r = row0 + rr, k = r - base;
-      float ga1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      float s = 0.f, ss = 0.f;
-      if (k < K) {
-        Raw8<T> dv[P], gv[P], hv[P];
-        bool okq[P], okk[P];
-        int rq[P], rk[P];
+  auto row_of = [&](int j) { return it.rho + j * dil; };
+  // gd stream: d and dL/d(hat a2) of one comb step
+  auto fetch_g = [&](int j, Raw8<T>& rd, Raw8<T>& rg, bool& ok, int& row) {
+    const int k = row_of(j);
+    ok = j >= 0 && k < K;
+    row = it.base + (ok ? k : 0);
+    rd.load(dd + (size_t)row * H + c * 8);
+    rg.load(ga2 + (size_t)row * H + c * 8);
+  };
+  auto finish_g = [&](const Raw8<T>& rd, const Raw8<T>& rg, bool ok, int row, bool count, float* gd) {
+    const float2 st = NK == NORM_GLN ? st2u : a.st2[row];
+    const float2 sm = NK == NORM_GLN ? sm2u : a.sm2[row];
 #pragma unroll
-        for (int p = 0; p < P; ++p) {
-          const int kq = k + a.pad - p * a.dil;   // output row whose tap p reads row k
-          const int kk = k - a.pad + p * a.dil;   // input row read by tap p of row k
-          okq[p] = kq >= 0 && kq < K;
-          okk[p] = kk >= 0 && kk < K;
-          rq[p] = base + (okq[p] ? kq : k);
-          rk[p] = base + (okk[p] ? kk : k);
-          dv[p].load(dd + (size_t)rq[p] * H + c * 8);
-          gv[p].load(ga2 + (size_t)rq[p] * H + c * 8);
-          hv[p].load(h1 + (size_t)rk[p] * H + c * 8);
-        }
-        float gn1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, gdo[8];
+    for (int e = 0; e < 8; ++e) {
+      const float x = rd[e];
+      const float ah = (prelu(x, al2) - st.x) * st.y;
+      const float ga = st.y * (rg[e] - sm.x - ah * sm.y);      // dL/da2
+      gd[e] = ok ? ga * prelu_dx(x, al2) : 0.f;
+      if (ok && count) calpha += ga * prelu_da(x);
+    }
+  };
+  // ah stream: hat a1 of one comb step
+  auto fetch_h = [&](int j, Raw8<T>& rh, bool& ok, int& row) {
+    const int k = row_of(j);
+    ok = j >= 0 && k < K;
+    row = it.base + (ok ? k : 0);
+    rh.load(h1 + (size_t)row * H + c * 8);
+  };
+  auto finish_h = [&](const Raw8<T>& rh, int row, float* ah) {
+    const float2 st = NK == NORM_GLN ? st1u : a.st1[row];
 #pragma unroll
-        for (int p = 0; p < P; ++p) {
-          const float2 st = NK == NORM_GLN ? st2u : a.st2[rq[p]];
-          const float2 sm = NK == NORM_GLN ? sm2u : a.sm2[rq[p]];
+    for (int e = 0; e < 8; ++e) ah[e] = (prelu(rh[e], al1) - st.x) * st.y;
+  };
+
+  float gdw[P][8], ahw[P][8];
+  bool ahok[P];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float x = dv[p][e];
-            const float ah = (prelu(x, al2) - st.x) * st.y;
-            const float ga = st.y * (gv[p][e] - sm.x - ah * sm.y);      // dL/da2
-            const float gd = ga * prelu_dx(x, al2);
-            gn1[e] += okq[p] ? cst(p, e) * gd : 0.f;
-            if (p == pown) {
-              gdo[e] = gd;
-              calpha += ga * prelu_da(x);
-            }
-          }
-        }
+  for (int i = 0; i < P - 1; ++i) {
+    Raw8<T> rd, rg, rh; bool ok, okh; int row, rowh;
+    const int sg = it.j0 + GT - P + 1 + i;
+    fetch_g(sg, rd, rg, ok, row);
+    fetch_h(it.j0 + AT - P + 1 + i, rh, okh, rowh);
+    finish_g(rd, rg, ok, row, sg >= it.j0 && sg < it.j1, gdw[i]);   // alpha2 term: own rows only
+    finish_h(rh, rowh, ahw[i]);
+    ahok[i] = okh;
+  }
+  Raw8<T> pd, pg, ph; bool pok, pokh; int prow, prowh;
+  fetch_g(it.j0 + GT, pd, pg, pok, prow);
+  fetch_h(it.j0 + AT, ph, pokh, prowh);
+  for (int j = it.j0; j < it.j1; ++j) {
+    Raw8<T> cd = pd, cgv = pg, ch = ph;
+    const bool cok = pok, cokh = pokh;
+    const int crow = prow, crowh = prowh;
+    if (j + 1 < it.j1) {
+      fetch_g(j + 1 + GT, pd, pg, pok, prow);
+      fetch_h(j + 1 + AT, ph, pokh, prowh);
+    }
+    finish_g(cd, cgv, cok, crow, j + GT < it.j1, gdw[P - 1]);   // halo rows are counted by their own segment
+    finish_h(ch, crowh, ahw[P - 1]);
+    ahok[P - 1] = cokh;
+    const int k = row_of(j);
+    float ga1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    float s = 0.f, ss = 0.f;
+    if (k < K) {
+      float gn1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-        for (int p = 0; p < P; ++p) {
-          const float2 st = NK == NORM_GLN ? st1u : a.st1[rk[p]];
+      for (int p = 0; p < P; ++p)
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float ah = (prelu(hv[p][e], al1) - st.x) * st.y;
-            cwd[p][e] += okk[p] ? gdo[e] * (ah * cst(P, e) + cst(P + 1, e)) : 0.f;
-            if (p == pown) {
-              cgam[e] += gn1[e] * ah;
-              cbet[e] += gn1[e];
-              ga1[e] = gn1[e] * cst(P, e);
-              s += ga1[e];
-              ss += ga1[e] * ah;
-            }
-          }
-        }
+        for (int e = 0; e < 8; ++e) gn1[e] += w[p][e] * gdw[P - 1 - p][e];
+#pragma unroll
+      for (int p = 0; p < P; ++p)
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          cwd[p][e] += ahok[p] ? gdw[P - 1 - POWN][e] * (ahw[p][e] * g1[e] + b1[e]) : 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float ah = ahw[POWN][e];
+        cgam[e] += gn1[e] * ah;
+        cbet[e] += gn1[e];
+        ga1[e] = gn1[e] * g1[e];
+        s += ga1[e];
+        ss += ga1[e] * ah;
       }
-      Vec8<T>::store(ga1o + (size_t)r * H + c * 8, ga1);
-      if constexpr (NK == NORM_GLN) {
-        ts += s;
-        tss += ss;
-      } else {
-        s = wave_sum_group(s, cg);
-        ss = wave_sum_group(ss, cg);
-        if (c == 0) a.slab1[r] = make_double2((double)s, (double)ss);
+    }
+    if (k < Kp) Vec8<T>::store(ga1o + (size_t)(it.base + k) * H + c * 8, ga1);
+    if constexpr (NK == NORM_GLN) {
+      ts += s;
+      tss += ss;
+    } else {
+      s = wave_sum_group(s, gm.cg);
+      ss = wave_sum_group(ss, gm.cg);
+      if (c == 0 && k < Kp) a.slab1[it.base + k] = make_double2((double)s, (double)ss);
+    }
+#pragma unroll
+    for (int i = 0; i < P - 1; ++i) {
+      ahok[i] = ahok[i + 1];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        gdw[i][e] = gdw[i + 1][e];
+        ahw[i][e] = ahw[i + 1][e];
       }
     }
   }
-  // ---- block reductions
+  // ---- workgroup reductions: column partials, alpha2, norm1 sums
+  const int cgn = gm.cg, nrl = 256 / cgn, rl = threadIdx.x / cgn;
   float* cs = a.col_slab + (size_t)blockIdx.x * dw_col_stride(a);
-  col_reduce8(buf, cgam, rl, c, nrl, cg, act, cs);
-  col_reduce8(buf, cbet, rl, c, nrl, cg, act, cs + H);
+  col_reduce8(buf, cgam, rl, c, nrl, cgn, true, cs);
+  col_reduce8(buf, cbet, rl, c, nrl, cgn, true, cs + H);
 #pragma unroll
   for (int p = 0; p < P; ++p) {
     // stored [H][P] to match the parameter layout [H,1,P]
-    if (act)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) buf[rl * H + c * 8 + e] = cwd[p][e];
+    for (int e = 0; e < 8; ++e) buf[rl * H + c * 8 + e] = cwd[p][e];
     __syncthreads();
-    for (int ch = tid; ch < H; ch += blockDim.x) {
+    for (int chn = threadIdx.x; chn < H; chn += blockDim.x) {
       float sacc = 0.f;
-      for (int q = 0; q < nrl; ++q) sacc += buf[q * H + ch];
-      cs[2 * H + ch * P + p] = sacc;
+      for (int q = 0; q < nrl; ++q) sacc += buf[q * H + chn];
+      cs[2 * H + chn * P + p] = sacc;
     }
     __syncthreads();
   }
   {
     double v3[3] = {(double)calpha, (double)ts, (double)tss};
     block_sum_d<3>(v3, red);
-    if (tid == 0) {
+    if (threadIdx.x == 0) {
       cs[(2 + P) * H] = (float)v3[0];
-      if constexpr (NK == NORM_GLN)
-        a.slab1[(size_t)m * (Kp / DW_RPB) + (row0 - base) / DW_RPB] = make_double2(v3[1], v3[2]);
+      if constexpr (NK == NORM_GLN) a.slab1[(size_t)it.m * gm.wgpu + it.wgi] = make_double2(v3[1], v3[2]);
     }
   }
 }
@@ -321,42 +393,45 @@ __global__ __launch_bounds__(256) void norm1_bwd_kernel(DwArgs a) {
 
 
 static hipError_t dw_check(const DwArgs& a) {
-  if (a.H % 8 != 0 || a.H / 8 > 256 || a.P < 1 || a.P > DW_MAXP || a.g.Kp % DW_RPB != 0) return hipErrorInvalidValue;
-  if (a.norm == NORM_CLN) {
-    const int cg = a.H / 8;
-    if (cg > 64 || (cg & (cg - 1))) return hipErrorInvalidValue;
-  }
+  const int cg = a.H / 8;
+  if (a.H % 8 != 0 || cg > 64 || (cg & (cg - 1)) || a.P < 1 || a.P > DW_MAXP || a.g.Kp % DW_RPB != 0 ||
+      a.dil < 1)
+    return hipErrorInvalidValue;
+  const int pown = a.pad / a.dil;
+  if (pown * a.dil != a.pad || (pown != a.P - 1 && pown != (a.P - 1) / 2)) return hipErrorInvalidValue;
   return hipSuccess;
 }
 
-#define CTN_DW_P_KERNEL(NAME)                                                                \
-  template <typename T, int NK, int P>                                                     \
-  static void NAME##_launch(const DwArgs& a, hipStream_t s) {                              \
-    hipLaunchKernelGGL((NAME##_kernel<T, NK, P>), dim3(dw_blocks(a)), dim3(256), 0, s, a); \
-  }                                                                                        \
-  template <typename T, int NK>                                                            \
-  static hipError_t NAME##_dispatch_p(const DwArgs& a, hipStream_t s) {                    \
-    switch (a.P) {                                                                         \
-      case 1: NAME##_launch<T, NK, 1>(a, s); break;                                        \
-      case 2: NAME##_launch<T, NK, 2>(a, s); break;                                        \
-      case 3: NAME##_launch<T, NK, 3>(a, s); break;                                        \
-      case 4: NAME##_launch<T, NK, 4>(a, s); break;                                        \
-      case 5: NAME##_launch<T, NK, 5>(a, s); break;                                        \
-      case 6: NAME##_launch<T, NK, 6>(a, s); break;                                        \
-      case 7: NAME##_launch<T, NK, 7>(a, s); break;                                        \
-      case 8: NAME##_launch<T, NK, 8>(a, s); break;                                        \
-      default: return hipErrorInvalidValue;                                                \
-    }                                                                                      \
-    return hipGetLastError();                                                              \
-  }                                                                                        \
-  hipError_t launch_##NAME(DType dt, const DwArgs& a, hipStream_t s) {                     \
-    hipError_t e = dw_check(a);                                                            \
-    if (e != hipSuccess) return e;                                                         \
-    if (dt == BF16)                                                                        \
-      return a.norm == NORM_GLN ? NAME##_dispatch_p<bf16raw, NORM_GLN>(a, s)               \
-                                : NAME##_dispatch_p<bf16raw, NORM_CLN>(a, s);              \
-    return a.norm == NORM_GLN ? NAME##_dispatch_p<float, NORM_GLN>(a, s)                   \
-                              : NAME##_dispatch_p<float, NORM_CLN>(a, s);                  \
+#define CTN_DW_P_KERNEL(NAME)                                                                  \
+  template <typename T, int NK, int P>                                                       \
+  static void NAME##_launch(const DwArgs& a, hipStream_t s) {                                \
+    const bool causal = a.pad / a.dil == P - 1 && P > 1 && (P - 1) != (P - 1) / 2;           \
+    if (causal) hipLaunchKernelGGL((NAME##_kernel<T, NK, P, true>), dim3(dw_blocks(a)), dim3(256), 0, s, a); \
+    else hipLaunchKernelGGL((NAME##_kernel<T, NK, P, false>), dim3(dw_blocks(a)), dim3(256), 0, s, a); \
+  }                                                                                          \
+  template <typename T, int NK>                                                              \
+  static hipError_t NAME##_dispatch_p(const DwArgs& a, hipStream_t s) {                      \
+    switch (a.P) {                                                                           \
+      case 1: NAME##_launch<T, NK, 1>(a, s); break;                                          \
+      case 2: NAME##_launch<T, NK, 2>(a, s); break;                                          \
+      case 3: NAME##_launch<T, NK, 3>(a, s); break;                                          \
+      case 4: NAME##_launch<T, NK, 4>(a, s); break;                                          \
+      case 5: NAME##_launch<T, NK, 5>(a, s); break;                                          \
+      case 6: NAME##_launch<T, NK, 6>(a, s); break;                                          \
+      case 7: NAME##_launch<T, NK, 7>(a, s); break;                                          \
+      case 8: NAME##_launch<T, NK, 8>(a, s); break;                                          \
+      default: return hipErrorInvalidValue;                                                  \
+    }                                                                                        \
+    return hipGetLastError();                                                                \
+  }                                                                                          \
+  hipError_t launch_##NAME(DType dt, const DwArgs& a, hipStream_t s) {                       \
+    hipError_t e = dw_check(a);                                                              \
+    if (e != hipSuccess) return e;                                                           \
+    if (dt == BF16)                                                                          \
+      return a.norm == NORM_GLN ? NAME##_dispatch_p<bf16raw, NORM_GLN>(a, s)                 \
+                                : NAME##_dispatch_p<bf16raw, NORM_CLN>(a, s);                \
+    return a.norm == NORM_GLN ? NAME##_dispatch_p<float, NORM_GLN>(a, s)                     \
+                              : NAME##_dispatch_p<float, NORM_CLN>(a, s);                    \
   }
 
 CTN_DW_P_KERNEL(dw_fwd)
@@ -365,7 +440,7 @@ CTN_DW_P_KERNEL(dw_bwd)
 hipError_t launch_norm1_bwd(DType dt, const DwArgs& a, hipStream_t s) {
   hipError_t e = dw_check(a);
   if (e != hipSuccess) return e;
-  const dim3 grid(dw_blocks(a)), blk(256);
+  const dim3 grid(ew_blocks(a)), blk(256);
   if (dt == BF16) {
     if (a.norm == NORM_GLN) hipLaunchKernelGGL((norm1_bwd_kernel<bf16raw, NORM_GLN>), grid, blk, 0, s, a);
     else hipLaunchKernelGGL((norm1_bwd_kernel<bf16raw, NORM_CLN>), grid, blk, 0, s, a);

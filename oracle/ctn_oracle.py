@@ -330,7 +330,7 @@ def train_step(cfg: Cfg, params, mixture, source, lengths, lr=1e-3, max_norm=5.0
     torch.nn.utils.clip_grad_norm_(plist, max_norm)
     opt = torch.optim.Adam(plist, lr=lr)
     opt.step()
-    return float(loss), {n: leaves[n].detach().clone() for n, _ in param_shapes(cfg)}
+    return float(loss.detach()), {n: leaves[n].detach().clone() for n, _ in param_shapes(cfg)}
 
 
 def fwd_bwd(cfg: Cfg, params, mixture, source, lengths):

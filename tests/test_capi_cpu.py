@@ -1,0 +1,101 @@
+"""C-ABI library checks that need no GPU: it loads, reports its ABI, exports
+every symbol include/ctn.h declares, and validates arguments (error codes and
+messages) before touching the device."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "ctn.h")
+
+
+@pytest.fixture(scope="module")
+def lib():
+    import ctn_lib as L
+    if not os.path.exists(L.LIB_PATH):
+        pytest.fail(f"{L.LIB_PATH} not built (run make / __graft_entry__.build())")
+    return L.load()
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(ctn_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_entry_points():
+    names = declared_functions()
+    for must in ("ctn_tblock_forward", "ctn_tblock_backward", "ctn_encoder_forward", "ctn_encoder_backward",
+                 "ctn_decoder_forward", "ctn_decoder_backward", "ctn_pit_forward", "ctn_pit_backward"):
+        assert must in names
+
+
+def test_every_declared_symbol_exported(lib):
+    import ctn_lib as L
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    assert set(declared_functions()) == set(L.EXPORTED_SYMBOLS), "ctypes signature table out of sync with ctn.h"
+
+
+def test_abi_and_padding(lib):
+    import ctn_lib as L
+    assert lib.ctn_abi_version() == L.ABI_VERSION
+    assert lib.ctn_padded_frames(3199) == 3200
+    assert lib.ctn_padded_frames(128) == 128
+    assert lib.ctn_padded_frames(7999) == 8064
+
+
+def _desc(**kw):
+    import ctn_lib as L
+    d = dict(M=2, K=3199, Kp=3200, B=256, H=512, P=3, dilation=4, causal=0, norm_type=0, dtype=1)
+    d.update(kw)
+    return L.TBlockDesc(**d)
+
+
+def test_tblock_validation(lib):
+    import ctn_lib as L
+    ok = _desc()
+    assert lib.ctn_tblock_workspace_bytes(ctypes.byref(ok), 0) > 0
+    assert lib.ctn_tblock_workspace_bytes(ctypes.byref(ok), 1) > lib.ctn_tblock_workspace_bytes(ctypes.byref(ok), 0)
+    assert lib.ctn_tblock_stats_floats(ctypes.byref(ok)) == 4 * 2
+    assert lib.ctn_tblock_stats_floats(ctypes.byref(_desc(norm_type=1))) == 4 * 2 * 3200
+    cases = [(_desc(Kp=3199), L.CtnLibraryError, "multiple of 128"),
+             (_desc(norm_type=2), None, "BN"),
+             (_desc(P=2), None, "odd P"),
+             (_desc(B=100), None, "multiples of 8")]
+    for d, _, msg in cases:
+        assert lib.ctn_tblock_workspace_bytes(ctypes.byref(d), 0) == 0
+        rc = lib.ctn_tblock_forward(ctypes.byref(d), None, None, None, None, None, 0, None)
+        assert rc in (1, 2)
+        assert msg in lib.ctn_last_error().decode()
+
+
+def test_forward_rejects_null_and_small_workspace(lib):
+    import ctn_lib as L
+    d = _desc()
+    p = L.TBlockParams()
+    sv = L.TBlockSaved()
+    assert lib.ctn_tblock_forward(ctypes.byref(d), ctypes.byref(p), None, None, ctypes.byref(sv), None, 0, None) == 1
+    assert lib.ctn_pit_forward(None, None, None, None, None, None, None, None, None, None, 0, None) == 1
+    pd = L.PitDesc(2, 5, 100)
+    assert lib.ctn_pit_workspace_bytes(ctypes.byref(pd)) == 0          # C > 4 unsupported
+
+
+def test_codec_validation(lib):
+    import ctn_lib as L
+    good = L.CodecDesc(M=2, T=32000, K=3199, Kp=3200, N=256, L=20, B=256, C=2, mask_type=0, dtype=1)
+    assert lib.ctn_encoder_workspace_bytes(ctypes.byref(good), 1) > 0
+    assert lib.ctn_decoder_workspace_bytes(ctypes.byref(good), 1) > 0
+    bad = L.CodecDesc(M=2, T=32000, K=3000, Kp=3072, N=256, L=20, B=256, C=2, mask_type=0, dtype=1)
+    assert lib.ctn_encoder_workspace_bytes(ctypes.byref(bad), 0) == 0
+    rc = lib.ctn_encoder_forward(ctypes.byref(bad), *([None] * 8), None, 0, None)
+    assert rc == 1 and "K=3000" in lib.ctn_last_error().decode()
+
+
+def test_timer_off_by_default(lib):
+    tot, n = ctypes.c_double(1.0), ctypes.c_int(7)
+    assert lib.ctn_timer_read(ctypes.byref(tot), ctypes.byref(n)) == 0
+    assert n.value == 0 and tot.value == 0.0

@@ -1,0 +1,81 @@
+"""Multi-process data parallelism on CPU (gloo, world_size 2): the DDP gradient
+all-reduce over equal per-rank shards reproduces the single-process full-batch
+gradient of the reference loss (loss = -mean over the batch,
+DDP averages rank gradients), and the bench's max-over-ranks timing reduction.
+The model here is the CPU oracle wrapped in an nn.Module — the HIP path runs the
+same DDP wrapper on RCCL on the GPU box."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import ctn_oracle as O
+
+CFG = O.Cfg(N=16, L=8, B=8, H=16, P=3, X=2, R=1, C=2)
+
+
+class OracleModel(torch.nn.Module):
+    def __init__(self, params):
+        super().__init__()
+        self.names = [n for n, _ in O.param_shapes(CFG)]
+        self.p = torch.nn.ParameterList([torch.nn.Parameter(params[n].clone()) for n in self.names])
+
+    def forward(self, mix):
+        return O.model_forward(CFG, mix, {n: p for n, p in zip(self.names, self.p)})
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    params = O.init_params(CFG, 7)
+    mix, src = O.synth_batch(4, CFG.C, 400, 3)
+    lens = torch.tensor([400, 400, 400, 400])
+    shard = slice(rank * 2, rank * 2 + 2)
+    model = torch.nn.parallel.DistributedDataParallel(OracleModel(params))
+    est = model(mix[shard])
+    loss = O.cal_loss(src[shard], est, lens[shard])[0]
+    loss.backward()
+    grads = [p.grad.clone() for p in model.module.p]
+    t = torch.tensor([0.1 * (rank + 1)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)                  # bench.py timing reduction
+    q.put((rank, [g.numpy() for g in grads], float(t)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_ddp_two_ranks_match_full_batch():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort()
+    # full-batch reference in this process
+    params = O.init_params(CFG, 7)
+    mix, src = O.synth_batch(4, CFG.C, 400, 3)
+    _, _, _, grads = O.fwd_bwd(CFG, params, mix, src, torch.tensor([400] * 4))
+    for (_, g_rank, tmax) in res:
+        assert abs(tmax - 0.2) < 1e-12
+        for n, gr in zip([n for n, _ in O.param_shapes(CFG)], g_rank):
+            torch.testing.assert_close(torch.from_numpy(gr), grads[n], rtol=1e-4, atol=1e-6)
+    # both ranks hold identical gradients after the all-reduce
+    for a, b in zip(res[0][1], res[1][1]):
+        assert (a == b).all()
