@@ -171,7 +171,8 @@ TbLayout tb_layout(const ctn_tblock_desc* d, int backward, void* ws) {
   const size_t es = esize(d->dtype);
   const int G = tb_groups(d);
   GemmRows g1 = tb_gemm1(d);
-  L.parts1 = gemm_rows_tiles_per_group(g1);
+  const DType dtl = d->dtype == CTN_DTYPE_BF16 ? BF16 : F32;
+  L.parts1 = gemm_rows_tiles_per_group(dtl, g1);
   DwArgs da{};
   da.g = rg; da.H = d->H; da.P = d->P; da.norm = d->norm_type; da.dil = d->dilation; da.pad = tb_pad(d);
   L.parts2 = dw_parts_per_group(da);
@@ -188,8 +189,8 @@ TbLayout tb_layout(const ctn_tblock_desc* d, int backward, void* ws) {
     L.G1 = c.take<void>((size_t)rows * d->H * es);
     L.G2 = c.take<void>((size_t)rows * d->H * es);
     GemmRows ga = tb_gemm1(d);   // same geometry as gemm1 (Nout = H)
-    L.partsA = gemm_rows_tiles_per_group(ga);
-    L.rowtiles = gemm_rows_rowtiles(ga);
+    L.partsA = gemm_rows_tiles_per_group(dtl, ga);
+    L.rowtiles = gemm_rows_rowtiles(dtl, ga);
     L.slabA = c.take<double2>((size_t)G * L.partsA * sizeof(double2));
     L.colA = c.take<float>((size_t)L.rowtiles * 2 * d->H * sizeof(float));
     L.partsD = L.parts2;
@@ -235,8 +236,11 @@ extern "C" int ctn_tblock_forward(const ctn_tblock_desc* d, const ctn_tblock_par
   const void* w1 = p->w1;
   const void* w2 = p->w2;
   if (dt == BF16) {
-    CTN_HIP(launch_prep_weight(dt, p->w1, d->H, d->B, L.w1s, nullptr, s));
-    CTN_HIP(launch_prep_weight(dt, p->w2, d->B, d->H, L.w2s, nullptr, s));
+    PrepBatch pb{};
+    pb.d[0] = PrepDesc{p->w1, d->H, d->B, L.w1s, nullptr};
+    pb.d[1] = PrepDesc{p->w2, d->B, d->H, L.w2s, nullptr};
+    pb.nd = 2;
+    CTN_HIP(launch_prep_weights(dt, pb, s));
     w1 = L.w1s;
     w2 = L.w2s;
   }
@@ -293,8 +297,13 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
   const float2* st2 = st1 + G;
   const double cnt = d->norm_type == CTN_NORM_GLN ? (double)d->K * d->H : (double)d->H;
 
-  CTN_HIP(launch_prep_weight(dt, p->w2, d->B, d->H, nullptr, L.w2t, s));   // [H][B]
-  CTN_HIP(launch_prep_weight(dt, p->w1, d->H, d->B, nullptr, L.w1t, s));   // [B][H]
+  {
+    PrepBatch pb{};
+    pb.d[0] = PrepDesc{p->w2, d->B, d->H, nullptr, L.w2t};   // [H][B]
+    pb.d[1] = PrepDesc{p->w1, d->H, d->B, nullptr, L.w1t};   // [B][H]
+    pb.nd = 2;
+    CTN_HIP(launch_prep_weights(dt, pb, s));
+  }
 
   // (a) g_n2 = gy . W2 ; epilogue: norm2 backward element part -> G1 = g_n2*gamma2, sums, gamma2/beta2 partials
   GemmRows ga = tb_gemm1(d);

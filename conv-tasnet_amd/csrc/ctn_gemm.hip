@@ -12,6 +12,8 @@
 //
 // MFMA: bf16 storage -> v_mfma_f32_16x16x32_bf16; fp32 storage (parity mode)
 // -> v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 accumulate).
+#include <stdlib.h>
+
 #include "ctn_common.h"
 #include "ctn_kernels.h"
 
@@ -57,6 +59,16 @@ template <> struct Chunk<bf16raw> {
 
 CTN_DEV u128 zero128() { u128 z; z.x = z.y = z.z = z.w = 0u; return z; }
 
+// XCD-aware bijective remap (cdna_hip_programming.md §5 T1): workgroups are
+// dealt round-robin over the 8 XCDs, so hardware id b runs on XCD b % 8; give
+// each XCD a contiguous range of logical tile ids so neighbouring tiles (which
+// share an operand panel) hit the same L2.  Speed only — correctness never
+// depends on placement.
+CTN_DEV int xcd_remap(int b, int n) {
+  const int x = b % 8, q = n / 8, r = n % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
 // op(v) for E consecutive channels starting at c0 of frame row `row`
 template <typename T, int OPK, int NK>
 CTN_DEV u128 apply_op(u128 v, int row, int c0, int Kp, const RowOp& op) {
@@ -81,11 +93,27 @@ CTN_DEV u128 apply_op(u128 v, int row, int c0, int Kp, const RowOp& op) {
 // ===========================================================================
 // gemm_rows
 // ===========================================================================
-constexpr int RBM = 128, RBN = 128, RPITCH = 144;   // bytes per LDS row (128 + 16 pad)
+constexpr int RBN = 128, RPITCH = 128;   // bytes per LDS row; 16-B slots XOR-swizzled by (row & 7)
 
-template <typename T, int OPK, int NK, int EPI>
+// LDS byte offset of 16-byte slot `kc` (0..7) of tile row `r`: conflict-free for the
+// ds_read_b128 fragment reads (16 rows x one slot) and the row-wise staging writes
+CTN_DEV int rslot(int r, int kc) { return r * RPITCH + ((kc ^ (r & 7)) << 4); }
+
+// Tile RBM frame rows x RBN output channels, 4 waves (2 x 2), each wave
+// (RBM/2) x 64 of 16x16 MFMA tiles; k-steps of 128 bytes, register-staged with
+// the A-operand transform applied on the way into LDS.
+constexpr int CPITCH = RBN + 4;   // floats per row of the fp32 C staging tile (epilogue)
+
+template <int RBM> struct RowsLds {
+  static constexpr int tiles = (RBM + RBN) * RPITCH;
+  static constexpr int ctile = RBM * CPITCH * 4;
+  static constexpr int bytes = (tiles > ctile ? tiles : ctile) + 4096;
+};
+
+template <typename T, int OPK, int NK, int EPI, int RBM>
 __global__ __launch_bounds__(256) void gemm_rows_kernel(GemmRows p) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * RBM * RPITCH];
+  __shared__ __attribute__((aligned(16))) char smem[RowsLds<RBM>::bytes];
+  constexpr int JT = RBM / 32;   // 16-row MFMA tiles per wave
   constexpr int E = Chunk<T>::E;              // elements per 16 B
   constexpr int BK = 128 / sizeof(T);         // elements per k-step (128 B per row)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -93,7 +121,7 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(GemmRows p) {
   const int lr = lane & 15, lg = lane >> 4;
 
   const int ncol = (p.Nout + RBN - 1) / RBN;
-  const int bid = blockIdx.x;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int coltile = bid % ncol, rowtile = bid / ncol;
   const int row0 = rowtile * RBM, col0 = coltile * RBN;
 
@@ -101,40 +129,60 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(GemmRows p) {
   const T* W = reinterpret_cast<const T*>(p.W);
   char* sA = smem;
   char* sW = smem + RBM * RPITCH;
+  constexpr int NA = RBM / 32;   // A chunks (16 B) per thread per k-step
 
-  u128 ra[4], rw[4];
+  u128 ra[NA], rw[4];
   auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int c = tid + 256 * i, r = c >> 3, kc = c & 7;
+      const int k = k0 + kc * E;
+      ra[i] = zero128();
+      if (k < p.Kred) ra[i] = *reinterpret_cast<const u128*>(A + (size_t)(row0 + r) * p.lda + k);
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int c = tid + 256 * i, r = c >> 3, kc = c & 7;
       const int k = k0 + kc * E;
-      ra[i] = zero128();
       rw[i] = zero128();
-      if (k < p.Kred) {
-        ra[i] = *reinterpret_cast<const u128*>(A + (size_t)(row0 + r) * p.lda + k);
-        if (col0 + r < p.Nout)
-          rw[i] = *reinterpret_cast<const u128*>(W + (size_t)(col0 + r) * p.ldw + k);
-      }
+      if (k < p.Kred && col0 + r < p.Nout) rw[i] = *reinterpret_cast<const u128*>(W + (size_t)(col0 + r) * p.ldw + k);
     }
   };
   auto swrite = [&](int k0) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NA; ++i) {
       const int c = tid + 256 * i, r = c >> 3, kc = c & 7;
       const int k = k0 + kc * E;
       u128 va = ra[i];
       if constexpr (OPK != OP_PLAIN)
         if (k < p.Kred) va = apply_op<T, OPK, NK>(va, row0 + r, k, p.g.Kp, p.aop);
-      *reinterpret_cast<u128*>(sA + r * RPITCH + kc * 16) = va;
-      *reinterpret_cast<u128*>(sW + r * RPITCH + kc * 16) = rw[i];
+      *reinterpret_cast<u128*>(sA + rslot(r, kc)) = va;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + 256 * i, r = c >> 3, kc = c & 7;
+      *reinterpret_cast<u128*>(sW + rslot(r, kc)) = rw[i];
     }
   };
 
-  f32x4_t acc[4][4];
+  f32x4_t acc[4][JT];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < JT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // epilogue operand (residual / pre-activation) prefetched now, consumed after the k loop:
+  // thread owns output chunks c = tid + 256*i -> row c/16, 8 columns (c%16)*8
+  constexpr int NC = RBM * RBN / 8 / 256;
+  const T* Rp = reinterpret_cast<const T*>(p.R);
+  Raw8<T> rpre[NC];
+  if constexpr (EPI == EPI_RESID || EPI == EPI_NORM_BWD) {
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const int c = tid + 256 * i, r = c >> 4, n = col0 + (c & 15) * 8;
+      if (n < p.Nout) rpre[i].load(Rp + (size_t)(row0 + r) * p.ldr + n);
+    }
+  }
 
   const int nk = (p.Kred + BK - 1) / BK;
   gload(0);
@@ -145,18 +193,18 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(GemmRows p) {
     if (kt + 1 < nk) gload((kt + 1) * BK);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      u128 wf[4], af[4];
+      u128 wf[4], af[JT];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        wf[i] = *reinterpret_cast<const u128*>(sW + (wc * 64 + i * 16 + lr) * RPITCH + kk * 64 + lg * 16);
+        wf[i] = *reinterpret_cast<const u128*>(sW + rslot(wc * 64 + i * 16 + lr, kk * 4 + lg));
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        af[j] = *reinterpret_cast<const u128*>(sA + (wr * 64 + j * 16 + lr) * RPITCH + kk * 64 + lg * 16);
+      for (int j = 0; j < JT; ++j)
+        af[j] = *reinterpret_cast<const u128*>(sA + rslot(wr * (RBM / 2) + j * 16 + lr, kk * 4 + lg));
       if constexpr (sizeof(T) == 2) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
+          for (int j = 0; j < JT; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                 __builtin_bit_cast(bf16x8_t, wf[i]), __builtin_bit_cast(bf16x8_t, af[j]), acc[i][j], 0, 0, 0);
       } else {
@@ -166,7 +214,7 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(GemmRows p) {
           for (int i = 0; i < 4; ++i) {
             const uint32_t wv = s == 0 ? wf[i].x : s == 1 ? wf[i].y : s == 2 ? wf[i].z : wf[i].w;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
+            for (int j = 0; j < JT; ++j) {
               const uint32_t av = s == 0 ? af[j].x : s == 1 ? af[j].y : s == 2 ? af[j].z : af[j].w;
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(wv), __uint_as_float(av),
                                                                acc[i][j], 0, 0, 0);
@@ -178,76 +226,89 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(GemmRows p) {
   }
 
   // ------------------------------------------------------------------ epilogue
-  // lane holds C[row0 + wr*64 + j*16 + lr][col0 + wc*64 + i*16 + lg*4 + 0..3]
-  T* Cp = reinterpret_cast<T*>(p.C);
-  const T* Rp = reinterpret_cast<const T*>(p.R);
-  const int K = p.g.K, Kp = p.g.Kp;
-  float ts = 0.f, tss = 0.f;                 // gLN group partials (this thread)
-  float rs[4] = {0, 0, 0, 0}, rss[4] = {0, 0, 0, 0};   // cLN per-row partials
-  float cg[4][4], cb[4][4];                  // NORM_BWD column partials
+  // 1) accumulators -> fp32 C tile in LDS (lane holds rows wr*(RBM/2)+j*16+lr, cols wc*64+i*16+lg*4..+3)
+  __syncthreads();
+  float* Cs = reinterpret_cast<float*>(smem);
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) { cg[i][q] = 0.f; cb[i][q] = 0.f; }
-  const float al = (EPI == EPI_PRELU_STATS || EPI == EPI_NORM_BWD) ? p.alpha[0] : 0.f;
-
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int r = row0 + wr * 64 + j * 16 + lr;
-    const bool valid = (r % Kp) < K;
-    float2 st = make_float2(0.f, 0.f);
-    if constexpr (EPI == EPI_NORM_BWD) st = p.stats[stat_index<NK>(r, Kp)];
+  for (int j = 0; j < JT; ++j)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int n = col0 + wc * 64 + i * 16 + lg * 4;
-      if (n >= p.Nout) continue;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if constexpr (EPI == EPI_STORE) {
-        if (!valid) v[0] = v[1] = v[2] = v[3] = 0.f;
-      } else if constexpr (EPI == EPI_PRELU_STATS) {
-        if (valid) {
+      const int r = wr * (RBM / 2) + j * 16 + lr, n = wc * 64 + i * 16 + lg * 4;
+      *reinterpret_cast<f32x4_t*>(Cs + r * CPITCH + n) = acc[i][j];
+    }
+  __syncthreads();
+  // 2) row-contiguous processing: 16 threads x 8 columns cover one 128-column tile row
+  T* Cp = reinterpret_cast<T*>(p.C);
+  const int K = p.g.K, Kp = p.g.Kp;
+  const float al = (EPI == EPI_PRELU_STATS || EPI == EPI_NORM_BWD) ? p.alpha[0] : 0.f;
+  const int cgi = tid & 15;                  // this thread's 8-column group (same for all its chunks)
+  float ts = 0.f, tss = 0.f;
+  float cgm[8], cbt[8], gam[8];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float a = prelu(v[q], al);
-            if constexpr (NK == NORM_GLN) { ts += a; tss += a * a; }
-            else { rs[j] += a; rss[j] += a * a; }
-          }
-        } else {
-          v[0] = v[1] = v[2] = v[3] = 0.f;
-        }
-      } else if constexpr (EPI == EPI_RESID) {
-        float x[4];
-        load4<T>(Rp + (size_t)r * p.ldr + n, x);
+  for (int e = 0; e < 8; ++e) {
+    cgm[e] = cbt[e] = 0.f;
+    gam[e] = 0.f;
+    if constexpr (EPI == EPI_NORM_BWD)
+      if (col0 + cgi * 8 + e < p.Nout) gam[e] = p.gamma[col0 + cgi * 8 + e];
+  }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = valid ? v[q] + x[q] : 0.f;
-      } else if constexpr (EPI == EPI_NORM_BWD) {
-        if (valid) {
-          float dv[4];
-          load4<T>(Rp + (size_t)r * p.ldr + n, dv);
+  for (int i = 0; i < NC; ++i) {
+    const int c = tid + 256 * i, rl = c >> 4, r = row0 + rl, n = col0 + cgi * 8;
+    const bool valid = (r % Kp) < K && n < p.Nout;   // columns past Nout: no output, no statistics
+    float v[8];
+    {
+      const f32x4_t lo = *reinterpret_cast<const f32x4_t*>(Cs + rl * CPITCH + cgi * 8);
+      const f32x4_t hi = *reinterpret_cast<const f32x4_t*>(Cs + rl * CPITCH + cgi * 8 + 4);
+      v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+      v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+    }
+    float s = 0.f, ss = 0.f;
+    if constexpr (EPI == EPI_STORE) {
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float ah = (prelu(dv[q], al) - st.x) * st.y;
-            const float gn = v[q];
-            const float ga = gn * p.gamma[n + q];
-            cg[i][q] += gn * ah;
-            cb[i][q] += gn;
-            if constexpr (NK == NORM_GLN) { ts += ga; tss += ga * ah; }
-            else { rs[j] += ga; rss[j] += ga * ah; }
-            v[q] = ga;
-          }
-        } else {
-          v[0] = v[1] = v[2] = v[3] = 0.f;
-        }
+      for (int e = 0; e < 8; ++e) v[e] = valid ? v[e] : 0.f;
+    } else if constexpr (EPI == EPI_PRELU_STATS) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float a2 = valid ? prelu(v[e], al) : 0.f;
+        s += a2;
+        ss += a2 * a2;
+        v[e] = valid ? v[e] : 0.f;
       }
-      store4<T>(Cp + (size_t)r * p.ldc + n, v);
+    } else if constexpr (EPI == EPI_RESID) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = valid ? v[e] + rpre[i][e] : 0.f;   // select: garbage never propagates
+    } else if constexpr (EPI == EPI_NORM_BWD) {
+      const float2 st = p.stats[stat_index<NK>(r, Kp)];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float ah = valid ? (prelu(rpre[i][e], al) - st.x) * st.y : 0.f;
+        const float gn = valid ? v[e] : 0.f;
+        const float ga = gn * gam[e];
+        cgm[e] += gn * ah;
+        cbt[e] += gn;
+        s += ga;
+        ss += ga * ah;
+        v[e] = ga;
+      }
+    }
+    if (n < p.Nout) Vec8<T>::store(Cp + (size_t)r * p.ldc + n, v);
+    if constexpr (EPI == EPI_PRELU_STATS || EPI == EPI_NORM_BWD) {
+      if constexpr (NK == NORM_GLN) {
+        ts += s;
+        tss += ss;
+      } else {
+        // per-row partial over this tile's 128 columns: the 16 lanes of one row
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) { s += __shfl_xor(s, o, 64); ss += __shfl_xor(ss, o, 64); }
+        if (cgi == 0) p.grp_slab[(size_t)r * ncol + coltile] = make_double2((double)s, (double)ss);
+      }
     }
   }
-
   if constexpr (EPI == EPI_PRELU_STATS || EPI == EPI_NORM_BWD) {
-    __syncthreads();   // LDS tiles are free now
-    double* red = reinterpret_cast<double*>(smem);
     if constexpr (NK == NORM_GLN) {
+      __syncthreads();
       double v2[2] = {(double)ts, (double)tss};
+      double* red = reinterpret_cast<double*>(smem + RowsLds<RBM>::bytes - 4096);
       block_sum_d<2>(v2, red);
       if (tid == 0) {
         const int tpu = (Kp / RBM) * ncol;    // tiles per utterance
@@ -255,73 +316,54 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(GemmRows p) {
         const int tiu = ((row0 % Kp) / RBM) * ncol + coltile;
         p.grp_slab[(size_t)m * tpu + tiu] = make_double2(v2[0], v2[1]);
       }
-    } else {
-      // per-row partial over this block's columns: reduce lanes with equal lr, then the two wc waves
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        rs[j] += __shfl_xor(rs[j], 16, 64); rs[j] += __shfl_xor(rs[j], 32, 64);
-        rss[j] += __shfl_xor(rss[j], 16, 64); rss[j] += __shfl_xor(rss[j], 32, 64);
-      }
-      float* fr = reinterpret_cast<float*>(smem);   // [2 wc][128 rows][2]
-      if (lg == 0) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int rl = wr * 64 + j * 16 + lr;
-          fr[(wc * RBM + rl) * 2 + 0] = rs[j];
-          fr[(wc * RBM + rl) * 2 + 1] = rss[j];
-        }
-      }
-      __syncthreads();
-      if (tid < RBM) {
-        const double a = (double)fr[tid * 2] + (double)fr[(RBM + tid) * 2];
-        const double b = (double)fr[tid * 2 + 1] + (double)fr[(RBM + tid) * 2 + 1];
-        p.grp_slab[(size_t)(row0 + tid) * ncol + coltile] = make_double2(a, b);
-      }
     }
   }
   if constexpr (EPI == EPI_NORM_BWD) {
+    // column partials: the 16 row-groups (tid >> 4) of each 8-column group
     __syncthreads();
+    float* fc = reinterpret_cast<float*>(smem);   // [16][RBN][2]
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float a = cg[i][q], b = cb[i][q];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) { a += __shfl_xor(a, o, 64); b += __shfl_xor(b, o, 64); }
-        cg[i][q] = a; cb[i][q] = b;
-      }
-    float* fc = reinterpret_cast<float*>(smem) + 4 * RBM;   // [2 wr][128 cols][2], after the row scratch
-    if (lr == 0) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int cl = wc * 64 + i * 16 + lg * 4 + q;
-          fc[(wr * RBN + cl) * 2 + 0] = cg[i][q];
-          fc[(wr * RBN + cl) * 2 + 1] = cb[i][q];
-        }
+    for (int e = 0; e < 8; ++e) {
+      fc[((tid >> 4) * RBN + cgi * 8 + e) * 2 + 0] = cgm[e];
+      fc[((tid >> 4) * RBN + cgi * 8 + e) * 2 + 1] = cbt[e];
     }
     __syncthreads();
     if (tid < RBN && col0 + tid < p.Nout) {
-      const float a = fc[tid * 2] + fc[(RBN + tid) * 2];
-      const float b = fc[tid * 2 + 1] + fc[(RBN + tid) * 2 + 1];
+      float a = 0.f, b = 0.f;
+      for (int q = 0; q < 16; ++q) {
+        a += fc[(q * RBN + tid) * 2];
+        b += fc[(q * RBN + tid) * 2 + 1];
+      }
       p.col_slab[((size_t)rowtile * 2 + 0) * p.Nout + col0 + tid] = a;
       p.col_slab[((size_t)rowtile * 2 + 1) * p.Nout + col0 + tid] = b;
     }
   }
 }
 
-int gemm_rows_tiles_per_group(const GemmRows& p) {
-  const int ncol = (p.Nout + RBN - 1) / RBN;
-  return p.norm == NORM_GLN ? (p.g.Kp / RBM) * ncol : ncol;
+// rows per tile: 64 (more workgroups per CU to hide load latency on the short
+// k loops of this model) unless CTN_GEMM_BM=128 is set (A/B experiments)
+static int rows_bm() {
+  static int bm = 0;
+  if (!bm) {
+    const char* e = getenv("CTN_GEMM_BM");
+    bm = (e && atoi(e) == 128) ? 128 : 64;
+  }
+  return bm;
 }
-int gemm_rows_rowtiles(const GemmRows& p) { return (int)(p.g.rows() / RBM); }
+
+int gemm_rows_tiles_per_group(DType, const GemmRows& p) {
+  const int ncol = (p.Nout + RBN - 1) / RBN;
+  return p.norm == NORM_GLN ? (p.g.Kp / rows_bm()) * ncol : ncol;
+}
+int gemm_rows_rowtiles(DType, const GemmRows& p) { return (int)(p.g.rows() / rows_bm()); }
 
 template <typename T, int OPK, int NK, int EPI>
 static hipError_t launch_rows_t(const GemmRows& p, hipStream_t s) {
   const int ncol = (p.Nout + RBN - 1) / RBN;
-  const int nrow = (int)(p.g.rows() / RBM);
-  hipLaunchKernelGGL((gemm_rows_kernel<T, OPK, NK, EPI>), dim3(nrow * ncol), dim3(256), 0, s, p);
+  const int bm = rows_bm();
+  const int nrow = (int)(p.g.rows() / bm);
+  if (bm == 128) hipLaunchKernelGGL((gemm_rows_kernel<T, OPK, NK, EPI, 128>), dim3(nrow * ncol), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL((gemm_rows_kernel<T, OPK, NK, EPI, 64>), dim3(nrow * ncol), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 
@@ -356,7 +398,7 @@ static hipError_t dispatch_rows(const GemmRows& p, hipStream_t s) {
 }
 
 hipError_t launch_gemm_rows(DType dt, const GemmRows& p, hipStream_t s) {
-  if (p.g.Kp % RBM != 0 || p.Kred % 8 != 0 || p.Nout % 8 != 0) return hipErrorInvalidValue;
+  if (p.g.Kp % 128 != 0 || p.Kred % 8 != 0 || p.Nout % 8 != 0) return hipErrorInvalidValue;
   return dt == BF16 ? dispatch_rows<bf16raw>(p, s) : dispatch_rows<float>(p, s);
 }
 
@@ -365,9 +407,19 @@ hipError_t launch_gemm_rows(DType dt, const GemmRows& p, hipStream_t s) {
 // ===========================================================================
 constexpr int CBP = 128, CBQ = 128, CKR = 32;   // tile p x q, rows per k-step
 
+// LDS byte offset of element (row, col) of a [CKR][128] staging tile.  bf16: the
+// 288-B pitch puts the 4 rows of one transposed read 8 banks apart, and rows
+// with bit 3 set are XOR-shifted by 64 columns (32 banks) so the two 16-lane
+// groups of a 32-lane half never collide.
+template <typename T> CTN_DEV int cswz(int row, int col);
+
 template <typename T> struct ColsPitch;
 template <> struct ColsPitch<bf16raw> { static constexpr int v = 288; };   // 256 B row + 32 pad
 template <> struct ColsPitch<float> { static constexpr int v = 576; };     // 512 B row + 64 pad
+template <> CTN_DEV int cswz<bf16raw>(int row, int col) {
+  return row * ColsPitch<bf16raw>::v + ((col ^ (((row >> 3) & 1) << 6)) << 1);
+}
+template <> CTN_DEV int cswz<float>(int row, int col) { return row * ColsPitch<float>::v + (col << 2); }
 
 template <typename T, int OPA, int OPB, int NK>
 __global__ __launch_bounds__(256) void gemm_cols_kernel(GemmCols p) {
@@ -381,7 +433,8 @@ __global__ __launch_bounds__(256) void gemm_cols_kernel(GemmCols p) {
   const int lr = lane & 15, lg = lane >> 4;
 
   const int ntq = (p.Q + CBQ - 1) / CBQ, ntp = (p.P + CBP - 1) / CBP;
-  const int tile = blockIdx.x % (ntp * ntq), chunk = blockIdx.x / (ntp * ntq);
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = bid % (ntp * ntq), chunk = bid / (ntp * ntq);
   const int p0 = (tile / ntq) * CBP, q0 = (tile % ntq) * CBQ;
 
   const long rows = p.g.rows();
@@ -421,8 +474,8 @@ __global__ __launch_bounds__(256) void gemm_cols_kernel(GemmCols p) {
         if (ok && p0 + cc * E < p.P) va = apply_op<T, OPA, NK>(va, (int)r, p0 + cc * E, Kp, p.aop);
       if constexpr (OPB != OP_PLAIN)
         if (ok && q0 + cc * E < p.Q) vb = apply_op<T, OPB, NK>(vb, (int)r, q0 + cc * E, Kp, p.bop);
-      *reinterpret_cast<u128*>(sA + rl * PITCH + cc * 16) = va;
-      *reinterpret_cast<u128*>(sB + rl * PITCH + cc * 16) = vb;
+      *reinterpret_cast<u128*>(sA + cswz<T>(rl, cc * E)) = va;
+      *reinterpret_cast<u128*>(sB + cswz<T>(rl, cc * E)) = vb;
     }
   };
 
@@ -446,18 +499,18 @@ __global__ __launch_bounds__(256) void gemm_cols_kernel(GemmCols p) {
       for (int i = 0; i < 4; ++i) {
         const int col = wp * 64 + i * 16 + 4 * pp;
         s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) s16x4_t*)(sA + (8 * lg + q) * PITCH + col * 2));
+            (__attribute__((address_space(3))) s16x4_t*)(sA + cswz<T>(8 * lg + q, col)));
         s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) s16x4_t*)(sA + (8 * lg + 4 + q) * PITCH + col * 2));
+            (__attribute__((address_space(3))) s16x4_t*)(sA + cswz<T>(8 * lg + 4 + q, col)));
         af[i] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int col = wq * 64 + j * 16 + 4 * pp;
         s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) s16x4_t*)(sB + (8 * lg + q) * PITCH + col * 2));
+            (__attribute__((address_space(3))) s16x4_t*)(sB + cswz<T>(8 * lg + q, col)));
         s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) s16x4_t*)(sB + (8 * lg + 4 + q) * PITCH + col * 2));
+            (__attribute__((address_space(3))) s16x4_t*)(sB + cswz<T>(8 * lg + 4 + q, col)));
         bfr[j] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
 #pragma unroll

@@ -44,8 +44,8 @@ struct GemmRows {
   double2* grp_slab = nullptr;            // group partials
   float* col_slab = nullptr;              // EPI_NORM_BWD column partials [rowtiles][2][Nout]
 };
-int gemm_rows_tiles_per_group(const GemmRows& p);   // slab parts per group
-int gemm_rows_rowtiles(const GemmRows& p);
+int gemm_rows_tiles_per_group(DType dt, const GemmRows& p);   // slab parts per group
+int gemm_rows_rowtiles(DType dt, const GemmRows& p);
 hipError_t launch_gemm_rows(DType dt, const GemmRows& p, hipStream_t s);
 
 // ---- column GEMM (weight gradient): Cpart[chunk][p][q] = sum_r opA(A[r][p]) * opB(B[r][q])
@@ -81,6 +81,17 @@ hipError_t launch_slab_reduce(const SlabBatch& b, hipStream_t s);
 // fp32 weight [O][I] -> storage-type copy (Ws, [O][I]) and/or transpose (Wt, [I][O])
 hipError_t launch_prep_weight(DType dt, const float* W, int O, int I, void* Ws, void* Wt,
                               hipStream_t s);
+struct PrepDesc {
+  const float* W;
+  int O, I;
+  void* Ws;
+  void* Wt;
+};
+struct PrepBatch {
+  PrepDesc d[4];
+  int nd;
+};
+hipError_t launch_prep_weights(DType dt, const PrepBatch& pb, hipStream_t s);   // one launch
 
 // ---- depthwise + norm element-wise kernels ---------------------------------
 struct DwArgs {

@@ -509,26 +509,32 @@ hipError_t launch_stats_finalize(const double2* slab, int G, int nparts, double 
   return hipGetLastError();
 }
 
-// out[i] = sum_q src[q * pstride + i]: workgroup = 16 consecutive outputs x 16 part lanes,
-// fixed summation order (deterministic), fp64 accumulation
-constexpr int SR_E = 16, SR_Q = 16;
+// out[i] = sum_q src[q * pstride + i].  Workgroup = one 64-output tile of one
+// descriptor; wave w sums parts q = w, w+4, ... (lanes = 64 consecutive
+// outputs: 256-byte coalesced rows, loads unrolled 8 deep), then the 4 wave
+// partials are combined in a fixed order — deterministic, fp64 accumulation.
 __global__ __launch_bounds__(256) void slab_reduce_kernel(SlabBatch b) {
-  __shared__ double part[SR_Q][SR_E];
+  __shared__ double part[4][64];
   const SlabDesc d = b.d[blockIdx.y];
-  const int e = threadIdx.x % SR_E, q0 = threadIdx.x / SR_E;
-  for (int i0 = blockIdx.x * SR_E; i0 < d.n; i0 += gridDim.x * SR_E) {
-    const int i = i0 + e;
-    double sacc = 0.0;
-    if (i < d.n)
-      for (int q = q0; q < d.nparts; q += SR_Q) sacc += (double)d.src[(size_t)q * d.pstride + i];
-    part[q0][e] = sacc;
-    __syncthreads();
-    if (q0 == 0 && i < d.n) {
-      double t = 0.0;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int i0 = blockIdx.x * 64; i0 < d.n; i0 += gridDim.x * 64) {
+    const int i = i0 + lane;
+    double acc = 0.0;
+    if (i < d.n) {
+      const float* src = d.src + i;
+      int q = w;
+      for (; q + 28 < d.nparts; q += 32) {
+        float v[8];
 #pragma unroll
-      for (int qq = 0; qq < SR_Q; ++qq) t += part[qq][e];
-      d.dst[i] = (float)t;
+        for (int u = 0; u < 8; ++u) v[u] = src[(size_t)(q + 4 * u) * d.pstride];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += (double)v[u];
+      }
+      for (; q < d.nparts; q += 4) acc += (double)src[(size_t)q * d.pstride];
     }
+    part[w][lane] = acc;
+    __syncthreads();
+    if (w == 0 && i < d.n) d.dst[i] = (float)(((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane]);
     __syncthreads();
   }
 }
@@ -537,32 +543,42 @@ hipError_t launch_slab_reduce(const SlabBatch& b, hipStream_t s) {
   if (b.nd <= 0) return hipSuccess;
   int mx = 1;
   for (int i = 0; i < b.nd; ++i) mx = b.d[i].n > mx ? b.d[i].n : mx;
-  int gx = (mx + SR_E - 1) / SR_E;
-  if (gx > 2048) gx = 2048;
+  int gx = (mx + 63) / 64;
+  if (gx > 1024) gx = 1024;
   hipLaunchKernelGGL(slab_reduce_kernel, dim3(gx, b.nd), dim3(256), 0, s, b);
   return hipGetLastError();
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void prep_weight_kernel(const float* W, int O, int I, T* Ws, T* Wt) {
-  const long n = (long)O * I;
+__global__ __launch_bounds__(256) void prep_weight_kernel(PrepBatch pb) {
+  const PrepDesc d = pb.d[blockIdx.y];
+  const long n = (long)d.O * d.I;
+  T* Ws = reinterpret_cast<T*>(d.Ws);
+  T* Wt = reinterpret_cast<T*>(d.Wt);
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
-    const int o = (int)(i / I), j = (int)(i % I);
-    const float v = W[i];
+    const int o = (int)(i / d.I), j = (int)(i % d.I);
+    const float v = d.W[i];
     if (Ws) st1<T>(Ws + i, v);
-    if (Wt) st1<T>(Wt + (size_t)j * O + o, v);
+    if (Wt) st1<T>(Wt + (size_t)j * d.O + o, v);
   }
 }
 
-hipError_t launch_prep_weight(DType dt, const float* W, int O, int I, void* Ws, void* Wt, hipStream_t s) {
-  const long n = (long)O * I;
-  int g = (int)((n + 255) / 256);
-  if (g > 1024) g = 1024;
-  if (dt == BF16)
-    hipLaunchKernelGGL(prep_weight_kernel<bf16raw>, dim3(g), dim3(256), 0, s, W, O, I, (bf16raw*)Ws, (bf16raw*)Wt);
-  else
-    hipLaunchKernelGGL(prep_weight_kernel<float>, dim3(g), dim3(256), 0, s, W, O, I, (float*)Ws, (float*)Wt);
+hipError_t launch_prep_weights(DType dt, const PrepBatch& pb, hipStream_t s) {
+  if (pb.nd <= 0) return hipSuccess;
+  long mx = 1;
+  for (int i = 0; i < pb.nd; ++i) mx = (long)pb.d[i].O * pb.d[i].I > mx ? (long)pb.d[i].O * pb.d[i].I : mx;
+  int g = (int)((mx + 255) / 256);
+  if (g > 512) g = 512;
+  if (dt == BF16) hipLaunchKernelGGL(prep_weight_kernel<bf16raw>, dim3(g, pb.nd), dim3(256), 0, s, pb);
+  else hipLaunchKernelGGL(prep_weight_kernel<float>, dim3(g, pb.nd), dim3(256), 0, s, pb);
   return hipGetLastError();
+}
+
+hipError_t launch_prep_weight(DType dt, const float* W, int O, int I, void* Ws, void* Wt, hipStream_t s) {
+  PrepBatch pb{};
+  pb.d[0] = PrepDesc{W, O, I, Ws, Wt};
+  pb.nd = 1;
+  return launch_prep_weights(dt, pb, s);
 }
 
 }  // namespace ctn
