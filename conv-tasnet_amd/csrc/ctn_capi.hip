@@ -102,6 +102,11 @@ struct Carver {
   }
 };
 size_t esize(int dt) { return dt == CTN_DTYPE_BF16 ? 2 : 4; }
+// scratch floats of the two-level slab reduction for one (nparts, n) descriptor
+size_t sr_tmp(long nparts, long n) {
+  const long ns = (nparts + 63) / 64;
+  return ns > 1 ? (size_t)(ns * n) : 0;
+}
 }  // namespace
 
 extern "C" int ctn_abi_version(void) { return CTN_ABI_VERSION; }
@@ -144,7 +149,7 @@ struct TbLayout {
   // backward
   void *w1t, *w2t, *G1, *G2;
   double2 *slabA, *slabD;
-  float *colA, *colD, *alphaSlab, *cpart1, *cpart2;
+  float *colA, *colD, *alphaSlab, *cpart1, *cpart2, *srtmp;
   float2 *sums1, *sums2;
   int parts1, parts2, partsA, partsD, chunks1, chunks2, rowtiles;
   size_t bytes;
@@ -206,6 +211,11 @@ TbLayout tb_layout(const ctn_tblock_desc* d, int backward, void* ws) {
     gc.P = d->H; gc.Q = d->B;
     L.chunks1 = gemm_cols_default_chunks(gc);
     L.cpart1 = c.take<float>((size_t)L.chunks1 * d->B * d->H * sizeof(float));
+    const long HB = (long)d->H * d->B, dwb = dw_blocks(da);
+    const size_t ntmp = sr_tmp(L.chunks2, HB) + sr_tmp(L.chunks1, HB) + 2 * sr_tmp(L.rowtiles, d->H) +
+                        2 * sr_tmp(dwb, d->H) + sr_tmp(dwb, (long)d->H * d->P) + sr_tmp(dwb, 1) +
+                        sr_tmp(ew_blocks(da), 1);
+    L.srtmp = c.take<float>(ntmp * sizeof(float));
   }
   L.bytes = c.off + 256;
   return L;
@@ -369,7 +379,7 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
   sb.d[7] = SlabDesc{L.colD + (2 + d->P) * H, gr->alpha2, dwb, 1, dws};
   sb.d[8] = SlabDesc{L.alphaSlab, gr->alpha1, ew_blocks(da), 1, 1};
   sb.nd = 9;
-  CTN_HIP(launch_slab_reduce(sb, s));
+  CTN_HIP(launch_slab_reduce(sb, L.srtmp, s));
   return CTN_OK;
 }
 
@@ -405,7 +415,7 @@ static CodecArgs codec_args(const ctn_codec_desc* d) {
 namespace {
 struct EncLayout {
   void *wbs, *wbt, *gcln;
-  float *gpre, *colE, *slabU, *cpartB;
+  float *gpre, *colE, *slabU, *cpartB, *srtmp;
   int chunksB, nU, rowblocks;
   size_t bytes;
 };
@@ -429,6 +439,9 @@ EncLayout enc_layout(const ctn_codec_desc* d, int backward, void* ws) {
     gc.g = Rows{d->M, d->K, d->Kp}; gc.P = d->B; gc.Q = d->N;
     L.chunksB = gemm_cols_default_chunks(gc);
     L.cpartB = c.take<float>((size_t)L.chunksB * d->B * d->N * sizeof(float));
+    const size_t ntmp = sr_tmp(L.chunksB, (long)d->B * d->N) + 2 * sr_tmp(L.rowblocks, d->N) +
+                        sr_tmp(L.nU, (long)d->N * d->L);
+    L.srtmp = c.take<float>(ntmp * sizeof(float));
   }
   L.bytes = c.off + 256;
   return L;
@@ -515,7 +528,7 @@ extern "C" int ctn_encoder_backward(const ctn_codec_desc* d, const float* mixtur
   fo.col_slab = Ly.slabU;
   CTN_HIP(launch_frame_outer(dt, 0, fo, s));
   sb.d[sb.nd++] = SlabDesc{Ly.slabU, gU, Ly.nU, d->N * d->L, d->N * d->L};
-  CTN_HIP(launch_slab_reduce(sb, s));
+  CTN_HIP(launch_slab_reduce(sb, Ly.srtmp, s));
   return CTN_OK;
 }
 
@@ -525,7 +538,7 @@ extern "C" int ctn_encoder_backward(const ctn_codec_desc* d, const float* mixtur
 namespace {
 struct DecLayout {
   void *wms, *wmt, *gscore;
-  float *frames, *slabV, *cpartM;
+  float *frames, *slabV, *cpartM, *srtmp;
   int nV, chunksM;
   size_t bytes;
 };
@@ -550,6 +563,7 @@ DecLayout dec_layout(const ctn_codec_desc* d, int backward, bool with_mask_conv,
       L.chunksM = gemm_cols_default_chunks(gc);
       L.cpartM = c.take<float>((size_t)L.chunksM * CN * d->B * sizeof(float));
     }
+    L.srtmp = c.take<float>((sr_tmp(L.nV, (long)d->N * d->L) + sr_tmp(L.chunksM, (long)CN * d->B)) * sizeof(float));
   }
   L.bytes = c.off + 256;
   return L;
@@ -634,7 +648,7 @@ extern "C" int ctn_decoder_backward(const ctn_codec_desc* d, const void* x_last,
     CTN_HIP(launch_gemm_cols(dt, gc, s));
     sb.d[sb.nd++] = SlabDesc{Ly.cpartM, gwm, Ly.chunksM, CN * d->B, CN * d->B};
   }
-  CTN_HIP(launch_slab_reduce(sb, s));
+  CTN_HIP(launch_slab_reduce(sb, Ly.srtmp, s));
   return CTN_OK;
 }
 

@@ -76,7 +76,8 @@ struct SlabBatch {
   SlabDesc d[12];
   int nd;
 };
-hipError_t launch_slab_reduce(const SlabBatch& b, hipStream_t s);
+size_t slab_reduce_tmp_floats(const SlabBatch& b);
+hipError_t launch_slab_reduce(const SlabBatch& b, float* tmp, hipStream_t s);   // tmp may be null (1 pass)
 
 // fp32 weight [O][I] -> storage-type copy (Ws, [O][I]) and/or transpose (Wt, [I][O])
 hipError_t launch_prep_weight(DType dt, const float* W, int O, int I, void* Ws, void* Wt,

@@ -509,44 +509,96 @@ hipError_t launch_stats_finalize(const double2* slab, int G, int nparts, double 
   return hipGetLastError();
 }
 
-// out[i] = sum_q src[q * pstride + i].  Workgroup = one 64-output tile of one
-// descriptor; wave w sums parts q = w, w+4, ... (lanes = 64 consecutive
-// outputs: 256-byte coalesced rows, loads unrolled 8 deep), then the 4 wave
-// partials are combined in a fixed order — deterministic, fp64 accumulation.
-__global__ __launch_bounds__(256) void slab_reduce_kernel(SlabBatch b) {
+// out[i] = sum_q src[q * pstride + i], deterministic, fp64 accumulation.
+// Workgroup = one 64-output tile x one slice of <= SR_SLICE parts of one
+// descriptor; wave w sums parts w, w+4, ... of the slice (lanes = 64
+// consecutive outputs: 256-byte rows, loads unrolled 8 deep); the 4 wave
+// partials combine in a fixed order.  Descriptors with more than one slice
+// write slice partials to `tmp` and a second pass sums the slices in order.
+constexpr int SR_SLICE = 64;
+
+struct SrJob {
+  const float* src;
+  float* dst;
+  int nparts, n, pstride, nslices;
+};
+struct SrBatch {
+  SrJob j[16];
+  int nj;
+};
+
+__global__ __launch_bounds__(256) void slab_reduce_kernel(SrBatch b) {
   __shared__ double part[4][64];
-  const SlabDesc d = b.d[blockIdx.y];
+  const SrJob d = b.j[blockIdx.z];
+  if ((int)blockIdx.y >= d.nslices) return;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int q0 = blockIdx.y * SR_SLICE;
+  const int q1 = d.nslices == 1 ? d.nparts : (q0 + SR_SLICE < d.nparts ? q0 + SR_SLICE : d.nparts);
+  float* out = d.nslices > 1 ? d.dst + (size_t)blockIdx.y * d.n : d.dst;
   for (int i0 = blockIdx.x * 64; i0 < d.n; i0 += gridDim.x * 64) {
     const int i = i0 + lane;
     double acc = 0.0;
     if (i < d.n) {
       const float* src = d.src + i;
-      int q = w;
-      for (; q + 28 < d.nparts; q += 32) {
+      int q = q0 + w;
+      for (; q + 28 < q1; q += 32) {
         float v[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) v[u] = src[(size_t)(q + 4 * u) * d.pstride];
 #pragma unroll
         for (int u = 0; u < 8; ++u) acc += (double)v[u];
       }
-      for (; q < d.nparts; q += 4) acc += (double)src[(size_t)q * d.pstride];
+      for (; q < q1; q += 4) acc += (double)src[(size_t)q * d.pstride];
     }
     part[w][lane] = acc;
     __syncthreads();
-    if (w == 0 && i < d.n) d.dst[i] = (float)(((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane]);
+    if (w == 0 && i < d.n) out[i] = (float)(((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane]);
     __syncthreads();
   }
 }
 
-hipError_t launch_slab_reduce(const SlabBatch& b, hipStream_t s) {
-  if (b.nd <= 0) return hipSuccess;
-  int mx = 1;
-  for (int i = 0; i < b.nd; ++i) mx = b.d[i].n > mx ? b.d[i].n : mx;
+static hipError_t sr_launch(const SrBatch& b, hipStream_t s) {
+  if (b.nj <= 0) return hipSuccess;
+  int mx = 1, ms = 1;
+  for (int i = 0; i < b.nj; ++i) {
+    mx = b.j[i].n > mx ? b.j[i].n : mx;
+    ms = b.j[i].nslices > ms ? b.j[i].nslices : ms;
+  }
   int gx = (mx + 63) / 64;
   if (gx > 1024) gx = 1024;
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3(gx, b.nd), dim3(256), 0, s, b);
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3(gx, ms, b.nj), dim3(256), 0, s, b);
   return hipGetLastError();
+}
+
+size_t slab_reduce_tmp_floats(const SlabBatch& b) {
+  size_t t = 0;
+  for (int i = 0; i < b.nd; ++i) {
+    const int ns = (b.d[i].nparts + SR_SLICE - 1) / SR_SLICE;
+    if (ns > 1) t += (size_t)ns * b.d[i].n;
+  }
+  return t;
+}
+
+hipError_t launch_slab_reduce(const SlabBatch& b, float* tmp, hipStream_t s) {
+  if (b.nd <= 0) return hipSuccess;
+  SrBatch p1{}, p2{};
+  size_t off = 0;
+  for (int i = 0; i < b.nd; ++i) {
+    const SlabDesc& d = b.d[i];
+    const int ns = (d.nparts + SR_SLICE - 1) / SR_SLICE;
+    if (ns <= 1 || !tmp) {
+      // single pass straight into dst (also the fallback when no scratch is given)
+      p2.j[p2.nj++] = SrJob{d.src, d.dst, d.nparts, d.n, d.pstride, 1};
+    } else {
+      float* t = tmp + off;
+      off += (size_t)ns * d.n;
+      p1.j[p1.nj++] = SrJob{d.src, t, d.nparts, d.n, d.pstride, ns};
+      p2.j[p2.nj++] = SrJob{t, d.dst, ns, d.n, d.n, 1};
+    }
+  }
+  hipError_t e = sr_launch(p1, s);
+  if (e != hipSuccess) return e;
+  return sr_launch(p2, s);
 }
 
 template <typename T>
