@@ -149,9 +149,9 @@ struct TbLayout {
   // backward
   void *w1t, *w2t, *G1, *G2;
   double2 *slabA, *slabD;
-  float *colA, *colD, *alphaSlab, *cpart1, *cpart2, *srtmp;
+  float *colD, *alphaSlab, *cpart1, *cpart2, *srtmp;
   float2 *sums1, *sums2;
-  int parts1, parts2, partsA, partsD, chunks1, chunks2, rowtiles;
+  int parts1, parts2, partsA, partsD, chunks1, chunks2;
   size_t bytes;
 };
 
@@ -159,12 +159,22 @@ int tb_pad(const ctn_tblock_desc* d) {
   return d->causal ? (d->P - 1) * d->dilation : (d->P - 1) * d->dilation / 2;
 }
 
-GemmRows tb_gemm1(const ctn_tblock_desc* d) {   // x[.,B] -> h1[.,H]
+// The two H-output GEMMs of a block, with everything but the data pointers
+// filled in: the slab sizing in tb_layout queries exactly what is launched.
+GemmRows tb_gemm1(const ctn_tblock_desc* d) {   // forward x[.,B] -> h1[.,H], PReLU statistics
   GemmRows g{};
   g.g = Rows{d->M, d->K, d->Kp};
   g.Kred = d->B;
   g.Nout = d->H;
   g.norm = d->norm_type;
+  g.lda = d->B; g.ldw = d->B; g.ldc = d->H;
+  g.epi = EPI_PRELU_STATS;
+  return g;
+}
+GemmRows tb_gemmA(const ctn_tblock_desc* d) {   // backward g_n2 = gy . W2, norm-2 backward epilogue
+  GemmRows g = tb_gemm1(d);
+  g.epi = EPI_NORM_BWD;
+  g.ldr = d->H;
   return g;
 }
 
@@ -193,11 +203,9 @@ TbLayout tb_layout(const ctn_tblock_desc* d, int backward, void* ws) {
     L.w2t = c.take<void>((size_t)d->H * d->B * es);
     L.G1 = c.take<void>((size_t)rows * d->H * es);
     L.G2 = c.take<void>((size_t)rows * d->H * es);
-    GemmRows ga = tb_gemm1(d);   // same geometry as gemm1 (Nout = H)
+    GemmRows ga = tb_gemmA(d);
     L.partsA = gemm_rows_tiles_per_group(dtl, ga);
-    L.rowtiles = gemm_rows_rowtiles(dtl, ga);
     L.slabA = c.take<double2>((size_t)G * L.partsA * sizeof(double2));
-    L.colA = c.take<float>((size_t)L.rowtiles * 2 * d->H * sizeof(float));
     L.partsD = L.parts2;
     L.slabD = c.take<double2>((size_t)G * L.partsD * sizeof(double2));
     L.colD = c.take<float>((size_t)dw_blocks(da) * dw_col_stride(da) * sizeof(float));
@@ -212,8 +220,8 @@ TbLayout tb_layout(const ctn_tblock_desc* d, int backward, void* ws) {
     L.chunks1 = gemm_cols_default_chunks(gc);
     L.cpart1 = c.take<float>((size_t)L.chunks1 * d->B * d->H * sizeof(float));
     const long HB = (long)d->H * d->B, dwb = dw_blocks(da);
-    const size_t ntmp = sr_tmp(L.chunks2, HB) + sr_tmp(L.chunks1, HB) + 2 * sr_tmp(L.rowtiles, d->H) +
-                        2 * sr_tmp(dwb, d->H) + sr_tmp(dwb, (long)d->H * d->P) + sr_tmp(dwb, 1) +
+    const size_t ntmp = sr_tmp(L.chunks2, HB) + sr_tmp(L.chunks1, HB) + 4 * sr_tmp(dwb, d->H) +
+                        sr_tmp(dwb, (long)d->H * d->P) + sr_tmp(dwb, 1) +
                         sr_tmp(ew_blocks(da), 1);
     L.srtmp = c.take<float>(ntmp * sizeof(float));
   }
@@ -256,11 +264,10 @@ extern "C" int ctn_tblock_forward(const ctn_tblock_desc* d, const ctn_tblock_par
   }
   // 1x1 conv B->H, PReLU statistics for norm1
   GemmRows g1 = tb_gemm1(d);
-  g1.A = x; g1.lda = d->B;
-  g1.W = w1; g1.ldw = d->B;
-  g1.epi = EPI_PRELU_STATS;
+  g1.A = x;
+  g1.W = w1;
   g1.alpha = p->alpha1;
-  g1.C = sv->h1; g1.ldc = d->H;
+  g1.C = sv->h1;
   g1.grp_slab = L.slab1;
   {
     TimedScope ts(1, s);
@@ -315,14 +322,14 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
     CTN_HIP(launch_prep_weights(dt, pb, s));
   }
 
-  // (a) g_n2 = gy . W2 ; epilogue: norm2 backward element part -> G1 = g_n2*gamma2, sums, gamma2/beta2 partials
-  GemmRows ga = tb_gemm1(d);
-  ga.A = gy; ga.lda = d->B;
-  ga.W = L.w2t; ga.ldw = d->B;
-  ga.epi = EPI_NORM_BWD; ga.R = sv->d; ga.ldr = d->H;
+  // (a) G1 = g_n2 = gy . W2 ; epilogue: norm-2 backward sums of (g_n2*gamma2, g_n2*gamma2*hat a2)
+  GemmRows ga = tb_gemmA(d);
+  ga.A = gy;
+  ga.W = L.w2t;
+  ga.R = sv->d;
   ga.alpha = p->alpha2; ga.stats = st2; ga.gamma = p->gamma2;
-  ga.C = L.G1; ga.ldc = d->H;
-  ga.grp_slab = L.slabA; ga.col_slab = L.colA;
+  ga.C = L.G1;
+  ga.grp_slab = L.slabA;
   {
     TimedScope ts(3, s);
     CTN_HIP(launch_gemm_rows(dt, ga, s));
@@ -337,7 +344,8 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
   c2.bop.gamma = p->gamma2; c2.bop.beta = p->beta2; c2.bop.alpha = p->alpha2;
   c2.Cpart = L.cpart2; c2.nchunks = L.chunks2;
   CTN_HIP(launch_gemm_cols(dt, c2, s));
-  // (c) depthwise backward -> G2 = dL/d(hat a1), norm1 sums, column partials
+  // (c) depthwise backward -> G2 = dL/d(hat a1), norm1 sums, column partials (gamma1/beta1,
+  //     wd, gamma2/beta2, alpha2)
   DwArgs da{};
   da.g = rg; da.H = d->H; da.P = d->P; da.dil = d->dilation; da.pad = tb_pad(d); da.norm = d->norm_type;
   da.h1 = sv->h1; da.d = sv->d; da.st1 = st1; da.st2 = st2;
@@ -371,12 +379,12 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
   SlabBatch sb{};
   sb.d[0] = SlabDesc{L.cpart2, gr->w2, L.chunks2, HB, HB};
   sb.d[1] = SlabDesc{L.cpart1, gr->w1, L.chunks1, HB, HB};
-  sb.d[2] = SlabDesc{L.colA, gr->gamma2, L.rowtiles, H, 2 * H};
-  sb.d[3] = SlabDesc{L.colA + H, gr->beta2, L.rowtiles, H, 2 * H};
+  sb.d[2] = SlabDesc{L.colD + (2 + d->P) * H, gr->gamma2, dwb, H, dws};
+  sb.d[3] = SlabDesc{L.colD + (3 + d->P) * H, gr->beta2, dwb, H, dws};
   sb.d[4] = SlabDesc{L.colD, gr->gamma1, dwb, H, dws};
   sb.d[5] = SlabDesc{L.colD + H, gr->beta1, dwb, H, dws};
   sb.d[6] = SlabDesc{L.colD + 2 * H, gr->wd, dwb, H * d->P, dws};
-  sb.d[7] = SlabDesc{L.colD + (2 + d->P) * H, gr->alpha2, dwb, 1, dws};
+  sb.d[7] = SlabDesc{L.colD + (4 + d->P) * H, gr->alpha2, dwb, 1, dws};
   sb.d[8] = SlabDesc{L.alphaSlab, gr->alpha1, ew_blocks(da), 1, 1};
   sb.nd = 9;
   CTN_HIP(launch_slab_reduce(sb, L.srtmp, s));

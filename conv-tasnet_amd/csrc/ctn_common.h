@@ -59,6 +59,53 @@ template <> struct Vec8<bf16raw> {
   }
 };
 
+// 16-byte register value as a first-class vector: copies of it never become
+// memcpy's, so arrays of them stay in registers (a struct copy can keep an
+// alloca alive in scratch or LDS).
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+CTN_DEV v4u ldg16(const void* p) { return *reinterpret_cast<const v4u*>(p); }
+CTN_DEV void stg16(void* p, v4u v) { *reinterpret_cast<v4u*>(p) = v; }
+CTN_DEV void unpack_bf16x8(const v4u& v, float f[8]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(v[i] << 16);
+    f[2 * i + 1] = __uint_as_float(v[i] & 0xffff0000u);
+  }
+}
+CTN_DEV v4u pack_bf16x8v(const float f[8]) {
+  v4u v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = (uint32_t)f2bf(f[2 * i]) | ((uint32_t)f2bf(f[2 * i + 1]) << 16);
+  return v;
+}
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations
+// but NOT for its outstanding global loads/stores (__syncthreads()' release
+// fence would emit vmcnt(0) and drain the next tile's prefetch).
+CTN_DEV void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// 8 bf16 held in a 16-byte register value <-> 8 floats (no memory round trip)
+CTN_DEV void unpack_bf16x8(const u128& v, float f[8]) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+CTN_DEV u128 pack_bf16x8(const float f[8]) {
+  u128 v;
+  v.x = (uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16);
+  v.y = (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16);
+  v.z = (uint32_t)f2bf(f[4]) | ((uint32_t)f2bf(f[5]) << 16);
+  v.w = (uint32_t)f2bf(f[6]) | ((uint32_t)f2bf(f[7]) << 16);
+  return v;
+}
+
 // Raw 8-element vector: loaded as-is (bf16: 4 dwords, f32: 8 dwords) so many
 // loads can be in flight in few registers; unpacked to fp32 at the point of use.
 template <typename T> struct Raw8;

@@ -90,6 +90,33 @@ CTN_DEV u128 apply_op(u128 v, int row, int c0, int Kp, const RowOp& op) {
   }
 }
 
+// op(v) on a 16-byte register vector (bf16 x8 or f32 x4)
+template <typename T, int OPK>
+CTN_DEV v4u apply_op_v(v4u v, float2 st, const float* g, const float* b, float al) {
+  constexpr int E = Chunk<T>::E;
+  float f[E];
+  if constexpr (E == 8) {
+    unpack_bf16x8(v, f);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) f[e] = __uint_as_float(v[e]);
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    float x = f[e];
+    if constexpr (OPK == OP_PRELU_NORM) x = prelu(x, al);
+    f[e] = (x - st.x) * (st.y * g[e]) + b[e];
+  }
+  if constexpr (E == 8) {
+    return pack_bf16x8v(f);
+  } else {
+    v4u r;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) r[e] = __float_as_uint(f[e]);
+    return r;
+  }
+}
+
 // ===========================================================================
 // gemm_rows
 // ===========================================================================
@@ -243,10 +270,9 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(GemmRows p) {
   const float al = (EPI == EPI_PRELU_STATS || EPI == EPI_NORM_BWD) ? p.alpha[0] : 0.f;
   const int cgi = tid & 15;                  // this thread's 8-column group (same for all its chunks)
   float ts = 0.f, tss = 0.f;
-  float cgm[8], cbt[8], gam[8];
+  float gam[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    cgm[e] = cbt[e] = 0.f;
     gam[e] = 0.f;
     if constexpr (EPI == EPI_NORM_BWD)
       if (col0 + cgi * 8 + e < p.Nout) gam[e] = p.gamma[col0 + cgi * 8 + e];
@@ -284,11 +310,9 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(GemmRows p) {
         const float ah = valid ? (prelu(rpre[i][e], al) - st.x) * st.y : 0.f;
         const float gn = valid ? v[e] : 0.f;
         const float ga = gn * gam[e];
-        cgm[e] += gn * ah;
-        cbt[e] += gn;
         s += ga;
         ss += ga * ah;
-        v[e] = ga;
+        v[e] = gn;
       }
     }
     if (n < p.Nout) Vec8<T>::store(Cp + (size_t)r * p.ldc + n, v);
@@ -318,26 +342,6 @@ __global__ __launch_bounds__(256) void gemm_rows_kernel(GemmRows p) {
       }
     }
   }
-  if constexpr (EPI == EPI_NORM_BWD) {
-    // column partials: the 16 row-groups (tid >> 4) of each 8-column group
-    __syncthreads();
-    float* fc = reinterpret_cast<float*>(smem);   // [16][RBN][2]
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      fc[((tid >> 4) * RBN + cgi * 8 + e) * 2 + 0] = cgm[e];
-      fc[((tid >> 4) * RBN + cgi * 8 + e) * 2 + 1] = cbt[e];
-    }
-    __syncthreads();
-    if (tid < RBN && col0 + tid < p.Nout) {
-      float a = 0.f, b = 0.f;
-      for (int q = 0; q < 16; ++q) {
-        a += fc[(q * RBN + tid) * 2];
-        b += fc[(q * RBN + tid) * 2 + 1];
-      }
-      p.col_slab[((size_t)rowtile * 2 + 0) * p.Nout + col0 + tid] = a;
-      p.col_slab[((size_t)rowtile * 2 + 1) * p.Nout + col0 + tid] = b;
-    }
-  }
 }
 
 // rows per tile: 64 (more workgroups per CU to hide load latency on the short
@@ -351,11 +355,11 @@ static int rows_bm() {
   return bm;
 }
 
-int gemm_rows_tiles_per_group(DType, const GemmRows& p) {
+int gemm_rows_tiles_per_group(DType dt, const GemmRows& p) {
+  if (gemm_ws_eligible(dt, p)) return gemm_ws_group_parts(p);
   const int ncol = (p.Nout + RBN - 1) / RBN;
   return p.norm == NORM_GLN ? (p.g.Kp / rows_bm()) * ncol : ncol;
 }
-int gemm_rows_rowtiles(DType, const GemmRows& p) { return (int)(p.g.rows() / rows_bm()); }
 
 template <typename T, int OPK, int NK, int EPI>
 static hipError_t launch_rows_t(const GemmRows& p, hipStream_t s) {
@@ -399,6 +403,7 @@ static hipError_t dispatch_rows(const GemmRows& p, hipStream_t s) {
 
 hipError_t launch_gemm_rows(DType dt, const GemmRows& p, hipStream_t s) {
   if (p.g.Kp % 128 != 0 || p.Kred % 8 != 0 || p.Nout % 8 != 0) return hipErrorInvalidValue;
+  if (gemm_ws_eligible(dt, p)) return launch_gemm_ws(p, s);
   return dt == BF16 ? dispatch_rows<bf16raw>(p, s) : dispatch_rows<float>(p, s);
 }
 
@@ -424,7 +429,8 @@ template <> CTN_DEV int cswz<float>(int row, int col) { return row * ColsPitch<f
 template <typename T, int OPA, int OPB, int NK>
 __global__ __launch_bounds__(256) void gemm_cols_kernel(GemmCols p) {
   constexpr int PITCH = ColsPitch<T>::v;
-  __shared__ __attribute__((aligned(16))) char smem[2 * CKR * PITCH];
+  constexpr int STAGE = 2 * CKR * PITCH;         // one k-step: A tile then B tile
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   constexpr int E = Chunk<T>::E;
   constexpr int CPR = CBP * sizeof(T) / 16;      // 16-byte chunks per LDS row
   constexpr int NCH = CKR * CPR / 256;           // chunks per thread per operand
@@ -437,45 +443,64 @@ __global__ __launch_bounds__(256) void gemm_cols_kernel(GemmCols p) {
   const int tile = bid % (ntp * ntq), chunk = bid / (ntp * ntq);
   const int p0 = (tile / ntq) * CBP, q0 = (tile % ntq) * CBQ;
 
-  const long rows = p.g.rows();
-  const long rpc = (((rows + p.nchunks - 1) / p.nchunks + CKR - 1) / CKR) * CKR;   // rows per chunk, multiple of CKR
-  const long rbeg = chunk * rpc;
-  const long rend = rbeg + rpc < rows ? rbeg + rpc : rows;   // may be <= rbeg: empty chunk writes zeros
+  // 32-bit row arithmetic (M*Kp < 2^31; checked by the launcher): no 64-bit divisions
+  const int rows = (int)p.g.rows();
+  const int rpc = (((rows + p.nchunks - 1) / p.nchunks + CKR - 1) / CKR) * CKR;   // rows per chunk, multiple of CKR
+  const int rbeg = chunk * rpc;
+  const int rend = rbeg + rpc < rows ? rbeg + rpc : rows;   // may be <= rbeg: empty chunk writes zeros
+  const int nks = rend > rbeg ? (rend - rbeg) / CKR : 0;    // k-steps (rows is a multiple of CKR)
 
   const T* A = reinterpret_cast<const T*>(p.A);
   const T* B = reinterpret_cast<const T*>(p.B);
-  char* sA = smem;
-  char* sB = smem + CKR * PITCH;
   const int K = p.g.K, Kp = p.g.Kp;
 
-  u128 ra[NCH], rb[NCH];
-  auto gload = [&](long r0) {
+  // per-thread operand-transform constants: a thread's 16-byte column chunk cc0 is the
+  // same for all its chunks and k-steps, so gamma/beta are loaded once
+  const int cc0 = tid % CPR;
+  float ga_[E], ba_[E], gb_[E], bb_[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    ga_[e] = ba_[e] = gb_[e] = bb_[e] = 0.f;
+    if constexpr (OPA != OP_PLAIN)
+      if (p0 + cc0 * E + e < p.P) { ga_[e] = p.aop.gamma[p0 + cc0 * E + e]; ba_[e] = p.aop.beta[p0 + cc0 * E + e]; }
+    if constexpr (OPB != OP_PLAIN)
+      if (q0 + cc0 * E + e < p.Q) { gb_[e] = p.bop.gamma[q0 + cc0 * E + e]; bb_[e] = p.bop.beta[q0 + cc0 * E + e]; }
+  }
+  const float ala = OPA == OP_PRELU_NORM ? p.aop.alpha[0] : 0.f;
+  const float alb = OPB == OP_PRELU_NORM ? p.bop.alpha[0] : 0.f;
+  const bool pin = p0 + cc0 * E < p.P, qin = q0 + cc0 * E < p.Q;
+
+  // Two register sets, each one k-step of both operands, loaded two steps ahead;
+  // rows past the chunk end are clamped to its last step (never stored).
+  struct Set { v4u a[NCH], b[NCH]; float2 sa[NCH], sb[NCH]; };
+  auto gload = [&](Set& R, int ks) __attribute__((always_inline)) {
+    const int r0 = rbeg + (ks < nks ? ks : nks - 1) * CKR;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      const int c = tid + 256 * i, rl = c / CPR, cc = c % CPR;
-      const long r = r0 + rl;
-      ra[i] = zero128();
-      rb[i] = zero128();
-      if (r < rend && (int)(r % Kp) < K) {
-        const int pc = p0 + cc * E, qc = q0 + cc * E;
-        if (pc < p.P) ra[i] = *reinterpret_cast<const u128*>(A + (size_t)r * p.lda + pc);
-        if (qc < p.Q) rb[i] = *reinterpret_cast<const u128*>(B + (size_t)r * p.ldb + qc);
-      }
+      const int c = tid + 256 * i, rl = c / CPR;
+      const int r = r0 + rl;
+      // unconditional loads (clamped column; zeroed in swrite) keep the loop branch-free
+      R.a[i] = ldg16(A + (size_t)r * p.lda + (pin ? p0 + cc0 * E : 0));
+      R.b[i] = ldg16(B + (size_t)r * p.ldb + (qin ? q0 + cc0 * E : 0));
+      if constexpr (OPA != OP_PLAIN) R.sa[i] = p.aop.stats[stat_index<NK>(r, Kp)];
+      if constexpr (OPB != OP_PLAIN) R.sb[i] = p.bop.stats[stat_index<NK>(r, Kp)];
     }
   };
-  auto swrite = [&](long r0) {
+  auto swrite = [&](const Set& R, int ks, char* st) __attribute__((always_inline)) {
+    const int r0 = rbeg + ks * CKR;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      const int c = tid + 256 * i, rl = c / CPR, cc = c % CPR;
-      const long r = r0 + rl;
-      u128 va = ra[i], vb = rb[i];
-      const bool ok = r < rend && (int)(r % Kp) < K;
-      if constexpr (OPA != OP_PLAIN)
-        if (ok && p0 + cc * E < p.P) va = apply_op<T, OPA, NK>(va, (int)r, p0 + cc * E, Kp, p.aop);
-      if constexpr (OPB != OP_PLAIN)
-        if (ok && q0 + cc * E < p.Q) vb = apply_op<T, OPB, NK>(vb, (int)r, q0 + cc * E, Kp, p.bop);
-      *reinterpret_cast<u128*>(sA + cswz<T>(rl, cc * E)) = va;
-      *reinterpret_cast<u128*>(sB + cswz<T>(rl, cc * E)) = vb;
+      const int c = tid + 256 * i, rl = c / CPR;
+      const int r = r0 + rl;
+      const bool ok = r % Kp < K;   // padded frames contribute nothing
+      v4u va = R.a[i], vb = R.b[i];
+      if constexpr (OPA != OP_PLAIN) va = apply_op_v<T, OPA>(va, R.sa[i], ga_, ba_, ala);
+      if constexpr (OPB != OP_PLAIN) vb = apply_op_v<T, OPB>(vb, R.sb[i], gb_, bb_, alb);
+      const v4u z = v4u{0u, 0u, 0u, 0u};
+      va = ok && pin ? va : z;
+      vb = ok && qin ? vb : z;
+      stg16(st + cswz<T>(rl, cc0 * E), va);
+      stg16(st + CKR * PITCH + cswz<T>(rl, cc0 * E), vb);
     }
   };
 
@@ -485,12 +510,9 @@ __global__ __launch_bounds__(256) void gemm_cols_kernel(GemmCols p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  if (rbeg < rend) gload(rbeg);
-  for (long r0 = rbeg; r0 < rend; r0 += CKR) {
-    __syncthreads();
-    swrite(r0);
-    __syncthreads();
-    if (r0 + CKR < rend) gload(r0 + CKR);
+  auto compute = [&](const char* st) __attribute__((always_inline)) {
+    const char* sA = st;
+    const char* sB = st + CKR * PITCH;
     if constexpr (sizeof(T) == 2) {
       // transposed LDS reads: lane (g, 4q+pp) addresses row 8g+4h+q, columns 4pp..4pp+3
       const int q = lr >> 2, pp = lr & 3;
@@ -535,6 +557,31 @@ __global__ __launch_bounds__(256) void gemm_cols_kernel(GemmCols p) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfv[j], acc[i][j], 0, 0, 0);
       }
     }
+  };
+
+  // Pipeline: step ks is written into LDS buffer ks&1 from register set ks&1 (loaded
+  // two steps earlier), then that set reloads step ks+2; one LDS-only barrier per
+  // step (the other buffer was last read before the previous barrier).
+  if (nks > 0) {
+    Set R0, R1;
+    gload(R0, 0);
+    gload(R1, 1);
+    int ks = 0;
+    for (; ks + 1 < nks; ks += 2) {   // full pairs: the same loads trail every wait
+      swrite(R0, ks, smem);
+      gload(R0, ks + 2);
+      lds_barrier();
+      compute(smem);
+      swrite(R1, ks + 1, smem + STAGE);
+      gload(R1, ks + 3);
+      lds_barrier();
+      compute(smem + STAGE);
+    }
+    if (ks < nks) {   // odd tail
+      swrite(R0, ks, smem);
+      lds_barrier();
+      compute(smem);
+    }
   }
   // lane holds D[p = p0 + wp*64 + i*16 + lg*4 + q][q = q0 + wq*64 + j*16 + lr]
   float* Cp = p.Cpart + (size_t)chunk * p.P * p.Q;
@@ -578,7 +625,8 @@ static hipError_t dispatch_cols_nk(const GemmCols& p, hipStream_t s) {
 }
 
 hipError_t launch_gemm_cols(DType dt, const GemmCols& p, hipStream_t s) {
-  if (p.g.Kp % CKR != 0 || p.P % 8 != 0 || p.Q % 8 != 0 || p.nchunks < 1) return hipErrorInvalidValue;
+  if (p.g.Kp % CKR != 0 || p.P % 8 != 0 || p.Q % 8 != 0 || p.nchunks < 1 || p.g.rows() >= (1L << 31))
+    return hipErrorInvalidValue;
   const int nk = p.bop.kind != OP_PLAIN ? p.bop.norm : 0;
   if (dt == BF16)
     return nk == NORM_GLN ? dispatch_cols_nk<bf16raw, NORM_GLN>(p, s) : dispatch_cols_nk<bf16raw, NORM_CLN>(p, s);

@@ -37,16 +37,24 @@ struct GemmRows {
   int epi = EPI_STORE;
   void* C; int ldc;
   const void* R = nullptr; int ldr = 0;   // residual (EPI_RESID) or pre-activation (EPI_NORM_BWD)
+  // EPI_NORM_BWD: C = gn = A.W^T (the gradient w.r.t. the norm output, padded rows 0);
+  // group sums of (gn*gamma, gn*gamma*hat a) with hat a = (PReLU(R) - mean) * rstd.
+  // The gamma/beta gradients are accumulated by the depthwise backward kernel.
   const float* alpha = nullptr;           // PReLU alpha for the epilogue
   const float2* stats = nullptr;          // EPI_NORM_BWD forward stats
   const float* gamma = nullptr;           // EPI_NORM_BWD gamma
   int norm = 0;                           // NormKind for the epilogue statistics
   double2* grp_slab = nullptr;            // group partials
-  float* col_slab = nullptr;              // EPI_NORM_BWD column partials [rowtiles][2][Nout]
 };
-int gemm_rows_tiles_per_group(DType dt, const GemmRows& p);   // slab parts per group
-int gemm_rows_rowtiles(DType dt, const GemmRows& p);
+// Slab sizing must be queried with the same GemmRows (shape, operand op, epilogue,
+// strides) that is later launched: the kernel choice decides the part counts.
+int gemm_rows_tiles_per_group(DType dt, const GemmRows& p);   // grp_slab parts per group
 hipError_t launch_gemm_rows(DType dt, const GemmRows& p, hipStream_t s);
+// weight-stationary persistent kernel (ctn_gemm_ws.hip), chosen by launch_gemm_rows
+bool gemm_ws_eligible(DType dt, const GemmRows& p);
+int gemm_ws_grid(const GemmRows& p);
+int gemm_ws_group_parts(const GemmRows& p);
+hipError_t launch_gemm_ws(const GemmRows& p, hipStream_t s);
 
 // ---- column GEMM (weight gradient): Cpart[chunk][p][q] = sum_r opA(A[r][p]) * opB(B[r][q])
 struct GemmCols {
@@ -109,11 +117,11 @@ struct DwArgs {
   void* d_out;
   double2* slab2;                        // stats partial of prelu(d)
   // bwd
-  const void* ga2;                       // dL/d(hat a2) = g_n2 * gamma2
+  const void* ga2;                       // bwd: g_n2 = dL/d(norm2 output); dL/d(hat a2) = g_n2 * gamma2
   const float2* sm2;                     // (mean ga2, mean ga2*hat a2)
   void* ga1_out;                         // dL/d(hat a1)
   double2* slab1;                        // partial (S1, S2) of layer-1 norm backward
-  float* col_slab;                       // [blocks][H*(2+P)+4]: ggamma1, gbeta1, gwd, galpha2
+  float* col_slab;                       // [blocks][dw_col_stride]: ggamma1, gbeta1, gwd, ggamma2, gbeta2, galpha2
   const float2* sm1;                     // (ew) layer-1 sums
   void* gh1_out;                         // (ew) dL/dh1
   float* alpha_slab;                     // (ew) [blocks] galpha1 partials

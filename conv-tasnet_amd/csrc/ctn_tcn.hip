@@ -48,7 +48,8 @@ __host__ __device__ inline CombGeom comb_geom(const DwArgs& a) {
 int dw_blocks(const DwArgs& a) { return a.g.M * comb_geom(a).wgpu; }
 int dw_parts_per_group(const DwArgs& a) { return a.norm == NORM_GLN ? comb_geom(a).wgpu : 1; }
 int ew_blocks(const DwArgs& a) { return (int)(a.g.rows() / DW_RPB); }
-__host__ __device__ int dw_col_stride(const DwArgs& a) { return ((2 + a.P) * a.H + 4 + 3) & ~3; }
+// col_slab part layout: [ggamma1 H][gbeta1 H][gwd H*P][ggamma2 H][gbeta2 H][galpha2 1], padded to 4
+__host__ __device__ int dw_col_stride(const DwArgs& a) { return ((4 + a.P) * a.H + 1 + 3) & ~3; }
 
 template <int NK> CTN_DEV float2 ld_stat(const float2* s, int m, int row) {
   return NK == NORM_GLN ? s[m] : s[row];
@@ -200,19 +201,22 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
   float2 st1u = make_float2(0.f, 0.f), st2u = st1u, sm2u = st1u;
   if constexpr (NK == NORM_GLN) { st1u = a.st1[it.m]; st2u = a.st2[it.m]; sm2u = a.sm2[it.m]; }
 
-  float w[P][8], g1[8], b1[8];
+  float w[P][8], g1[8], b1[8], g2[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const int ch = c * 8 + e;
     g1[e] = a.gamma1[ch];
     b1[e] = a.beta1[ch];
+    g2[e] = a.gamma2[ch];
 #pragma unroll
     for (int p = 0; p < P; ++p) w[p][e] = a.wd[ch * P + p];
   }
-  float cgam[8], cbet[8], cwd[P][8];
+  // cgam/cbet: norm-1 affine gradients; cgam2/cbet2: norm-2 affine gradients
+  // (sum over own rows of g_n2 * hat a2 and of g_n2)
+  float cgam[8], cbet[8], cgam2[8], cbet2[8], cwd[P][8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    cgam[e] = cbet[e] = 0.f;
+    cgam[e] = cbet[e] = cgam2[e] = cbet2[e] = 0.f;
 #pragma unroll
     for (int p = 0; p < P; ++p) cwd[p][e] = 0.f;
   }
@@ -234,9 +238,14 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
     for (int e = 0; e < 8; ++e) {
       const float x = rd[e];
       const float ah = (prelu(x, al2) - st.x) * st.y;
-      const float ga = st.y * (rg[e] - sm.x - ah * sm.y);      // dL/da2
+      const float gn = rg[e];                                   // dL/d(norm2 output)
+      const float ga = st.y * (gn * g2[e] - sm.x - ah * sm.y);  // dL/da2
       gd[e] = ok ? ga * prelu_dx(x, al2) : 0.f;
-      if (ok && count) calpha += ga * prelu_da(x);
+      if (ok && count) {
+        calpha += ga * prelu_da(x);
+        cgam2[e] += gn * ah;
+        cbet2[e] += gn;
+      }
     }
   };
   // ah stream: hat a1 of one comb step
@@ -326,6 +335,8 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
   float* cs = a.col_slab + (size_t)blockIdx.x * dw_col_stride(a);
   col_reduce8(buf, cgam, rl, c, nrl, cgn, true, cs);
   col_reduce8(buf, cbet, rl, c, nrl, cgn, true, cs + H);
+  col_reduce8(buf, cgam2, rl, c, nrl, cgn, true, cs + (2 + P) * H);
+  col_reduce8(buf, cbet2, rl, c, nrl, cgn, true, cs + (3 + P) * H);
 #pragma unroll
   for (int p = 0; p < P; ++p) {
     // stored [H][P] to match the parameter layout [H,1,P]
@@ -343,7 +354,7 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
     double v3[3] = {(double)calpha, (double)ts, (double)tss};
     block_sum_d<3>(v3, red);
     if (threadIdx.x == 0) {
-      cs[(2 + P) * H] = (float)v3[0];
+      cs[(4 + P) * H] = (float)v3[0];
       if constexpr (NK == NORM_GLN) a.slab1[(size_t)it.m * gm.wgpu + it.wgi] = make_double2(v3[1], v3[2]);
     }
   }
