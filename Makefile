@@ -5,8 +5,12 @@ PKG      := conv-tasnet_amd
 SRC      := $(wildcard $(PKG)/csrc/*.hip)
 OBJ      := $(patsubst $(PKG)/csrc/%.hip,build/%.o,$(SRC))
 HDR      := $(wildcard $(PKG)/csrc/*.h) include/ctn.h
-CXXFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function -Iinclude
+CXXFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function -Iinclude $(DEVFLAGS)
 LIB      := $(PKG)/libctn_hip.so
+# device codegen: MFMA accumulators in VGPRs (no accvgpr copies in the epilogues);
+# IEEE mode off (no NaN-quieting canonicalisation before every min/max; the path
+# never relies on signalling-NaN semantics)
+DEVFLAGS := -mllvm -amdgpu-mfma-vgpr-form -mno-amdgpu-ieee -fno-honor-nans
 
 all: $(LIB)
 
@@ -21,3 +25,12 @@ clean:
 	rm -rf build $(LIB)
 
 .PHONY: all clean
+
+# bound-finding microbenchmarks (not part of the library): build/ws_bench_<bits>
+MB_EXPS := 0 1 2 3 4 8 12
+microbench: $(patsubst %,build/ws_bench_%,$(MB_EXPS))
+build/ws_bench_%: tools/microbench/ws_bench.hip $(PKG)/csrc/ctn_gemm_ws.hip $(HDR)
+	@mkdir -p build
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -Iinclude $(DEVFLAGS) -DCTN_WS_EXP=$* $< -o $@
+
+.PHONY: microbench

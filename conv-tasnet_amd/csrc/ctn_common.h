@@ -48,15 +48,7 @@ template <> struct Vec8<bf16raw> {
       v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
     }
   }
-  static CTN_DEV void store(bf16raw* p, const float v[8]) {
-    u128 a;
-    uint32_t w[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
-    a.x = w[0]; a.y = w[1]; a.z = w[2]; a.w = w[3];
-    *reinterpret_cast<u128*>(p) = a;
-  }
+  static CTN_DEV void store(bf16raw* p, const float v[8]);
 };
 
 // 16-byte register value as a first-class vector: copies of it never become
@@ -72,16 +64,19 @@ CTN_DEV void unpack_bf16x8(const v4u& v, float f[8]) {
     f[2 * i + 1] = __uint_as_float(v[i] & 0xffff0000u);
   }
 }
+// two floats -> one dword of 2 bf16 (round to nearest even): one v_cvt_pk_bf16_f32
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+CTN_DEV uint32_t pk_bf16(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{a, b}, bf16x2_t));
+}
 CTN_DEV v4u pack_bf16x8v(const float f[8]) {
-  v4u v;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) v[i] = (uint32_t)f2bf(f[2 * i]) | ((uint32_t)f2bf(f[2 * i + 1]) << 16);
-  return v;
+  return v4u{pk_bf16(f[0], f[1]), pk_bf16(f[2], f[3]), pk_bf16(f[4], f[5]), pk_bf16(f[6], f[7])};
 }
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations
 // but NOT for its outstanding global loads/stores (__syncthreads()' release
-// fence would emit vmcnt(0) and drain the next tile's prefetch).
+// fence would emit vmcnt(0) and drain the prefetch in flight).
 CTN_DEV void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -99,12 +94,13 @@ CTN_DEV void unpack_bf16x8(const u128& v, float f[8]) {
 }
 CTN_DEV u128 pack_bf16x8(const float f[8]) {
   u128 v;
-  v.x = (uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16);
-  v.y = (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16);
-  v.z = (uint32_t)f2bf(f[4]) | ((uint32_t)f2bf(f[5]) << 16);
-  v.w = (uint32_t)f2bf(f[6]) | ((uint32_t)f2bf(f[7]) << 16);
+  v.x = pk_bf16(f[0], f[1]);
+  v.y = pk_bf16(f[2], f[3]);
+  v.z = pk_bf16(f[4], f[5]);
+  v.w = pk_bf16(f[6], f[7]);
   return v;
 }
+CTN_DEV void Vec8<bf16raw>::store(bf16raw* p, const float v[8]) { stg16(p, pack_bf16x8v(v)); }
 
 // Raw 8-element vector: loaded as-is (bf16: 4 dwords, f32: 8 dwords) so many
 // loads can be in flight in few registers; unpacked to fp32 at the point of use.
@@ -135,8 +131,8 @@ template <> CTN_DEV void store4<float>(float* p, const float v[4]) {
 }
 template <> CTN_DEV void store4<bf16raw>(bf16raw* p, const float v[4]) {
   uint2 a;
-  a.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-  a.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+  a.x = pk_bf16(v[0], v[1]);
+  a.y = pk_bf16(v[2], v[3]);
   *reinterpret_cast<uint2*>(p) = a;
 }
 template <typename T> CTN_DEV void load4(const T* p, float v[4]);
@@ -184,6 +180,32 @@ template <typename V> CTN_DEV V wave_sum_stride(V v, int width) {
 template <typename V> CTN_DEV V wave_sum_group(V v, int width) {
   for (int o = width >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
+}
+
+// Wave64 sum with DPP row operations (no LDS traffic); the total is returned
+// wave-uniform (read from lane 63).
+template <int CTRL, int ROW_MASK> CTN_DEV float dpp_f(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, ROW_MASK, 0xF, false));
+}
+CTN_DEV float wave_sum_dpp(float v) {
+  v += dpp_f<0xB1, 0xF>(v);    // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E, 0xF>(v);    // quad_perm [2,3,0,1]
+  v += dpp_f<0x141, 0xF>(v);   // row_half_mirror
+  v += dpp_f<0x140, 0xF>(v);   // row_mirror: every lane holds its 16-lane row sum
+  v += dpp_f<0x142, 0xA>(v);   // row_bcast:15 into rows 1 and 3
+  v += dpp_f<0x143, 0xC>(v);   // row_bcast:31 into rows 2 and 3
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+
+// float2 (packed fp32: v_pk_add/mul/fma_f32 on gfx950) helpers
+CTN_DEV f32x2_t pmax(f32x2_t a, f32x2_t b) { return __builtin_elementwise_max(a, b); }
+CTN_DEV f32x2_t pmin(f32x2_t a, f32x2_t b) { return __builtin_elementwise_min(a, b); }
+CTN_DEV f32x2_t pfma(f32x2_t a, f32x2_t b, f32x2_t c) { return __builtin_elementwise_fma(a, b, c); }
+// PReLU of a pair with one shared alpha: max(x, a*x) when a <= 1, min(x, a*x) when a > 1
+// (both exact: the branch is chosen once per kernel, LE1 = (alpha <= 1))
+template <bool LE1> CTN_DEV f32x2_t prelu2(f32x2_t x, float a) {
+  const f32x2_t ax = x * a;
+  return LE1 ? pmax(x, ax) : pmin(x, ax);
 }
 
 // Block-wide sum of NV doubles; result valid in thread 0.  `red` must hold

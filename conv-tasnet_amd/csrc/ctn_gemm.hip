@@ -48,13 +48,7 @@ template <> struct Chunk<bf16raw> {
       f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
     }
   }
-  static CTN_DEV u128 pack(const float* f) {
-    uint32_t w[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      w[i] = (uint32_t)f2bf(f[2 * i]) | ((uint32_t)f2bf(f[2 * i + 1]) << 16);
-    u128 v; v.x = w[0]; v.y = w[1]; v.z = w[2]; v.w = w[3]; return v;
-  }
+  static CTN_DEV u128 pack(const float* f) { return pack_bf16x8(f); }
 };
 
 CTN_DEV u128 zero128() { u128 z; z.x = z.y = z.z = z.w = 0u; return z; }
