@@ -156,75 +156,115 @@ __global__ __launch_bounds__(256) void enc_bwd_rows_kernel(CodecArgs a) {
 }
 
 // ===========================================================================
-// frame_outer: out[n][l] partial over a chunk of frame rows
-//   mode 0 (encoder dU):  sum_r gpre[r][n] * x[m][kS + l]
-//   mode 1 (decoder dV):  sum_r sum_c (w[r][n] act_c(score[r][.][n])) * gest[m][c][kS + l]
-// workgroup = chunk of rows inside one utterance; thread = channel n (looped)
-// slab layout: [chunks][N][L]
+// frame_outer: weight gradients of the two framing convolutions
+//   mode 0 (encoder dU [N][L]):  sum_r gpre[r][n] * x[m][kS + l]
+//   mode 1 (decoder dV [L][N]):  sum_r sum_c (w[r][n] act_c(score[r][c][n])) * gest[m][c][kS + l]
+// Persistent: FO_WGS workgroups each sweep a contiguous run of FO_R-row chunks
+// (chunks never straddle utterances).  Per chunk the rows are staged into LDS
+// with 16-byte loads by all threads (mode 1 forms src = w * act(score) on the
+// way), together with the chunk's signal span; thread n then accumulates its
+// channel's L outputs from LDS across all of its chunks.  Padded frames stage
+// as zeros.  One fp32 partial per workgroup -> slab [FO_WGS][N*L].
 // ===========================================================================
-template <typename T, int MODE>
-__global__ __launch_bounds__(256) void frame_outer_kernel(CodecArgs a, int rows_per_chunk) {
+constexpr int FO_R = 16, FO_WGS = 512, FO_LMAX = 32;
+
+template <typename T, int MODE, int LT>   // LT: compile-time L (0: generic, <= FO_LMAX)
+__global__ __launch_bounds__(256) void frame_outer_kernel(CodecArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int N = a.N, L = a.L, S = a.S, C = MODE == 0 ? 1 : a.C, K = a.K, Kp = a.Kp;
-  const int chunks_per_utt = (Kp + rows_per_chunk - 1) / rows_per_chunk;
-  const int m = blockIdx.x / chunks_per_utt, ch = blockIdx.x % chunks_per_utt;
-  const int kb = ch * rows_per_chunk;
-  int ke = kb + rows_per_chunk;
-  if (ke > K) ke = K;
-  const int nk = ke > kb ? ke - kb : 0;
-  // signal samples for this chunk, per speaker: [C][nk*S + L]
-  const int span = rows_per_chunk * S + L;
-  for (int i = threadIdx.x; i < C * span; i += 256) {
-    const int cc = i / span, j = i % span;
-    const long t = (long)kb * S + j;
-    float v = 0.f;
-    if (MODE == 0) v = t < a.T ? a.mixture[(size_t)m * a.T + t] : 0.f;
-    else v = t < a.T ? a.gest[((size_t)m * a.C + cc) * a.T + t] : 0.f;
-    sm[i] = v;
-  }
-  __syncthreads();
+  constexpr int LL = LT ? LT : FO_LMAX;
+  const int N = a.N, L = LT ? LT : a.L, S = a.S, C = MODE == 0 ? 1 : a.C, K = a.K, Kp = a.Kp;
+  const int cg = N / 8;                               // 8-channel groups per row
+  const int span = FO_R * S + L;                      // signal samples of one chunk
+  float* srcs = sm;                                   // [FO_R][C][N]
+  float* sig = sm + FO_R * C * N;                     // [C][span]
+  const int nchunk = a.M * (Kp / FO_R);
+  const int c0 = (int)((long)nchunk * blockIdx.x / gridDim.x), c1 = (int)((long)nchunk * (blockIdx.x + 1) / gridDim.x);
   const T* w = reinterpret_cast<const T*>(a.w_rows);
   const T* sc = reinterpret_cast<const T*>(a.score);
-  float* out = a.col_slab + (size_t)blockIdx.x * N * L;
-  for (int n = threadIdx.x; n < N; n += 256) {
-    float acc[32];
+  constexpr int NPT = 2;                              // channels per thread (N <= 512)
+  float acc[NPT][LL];
 #pragma unroll
-    for (int l = 0; l < 32; ++l) acc[l] = 0.f;
-    for (int kk = 0; kk < nk; ++kk) {
-      const size_t r = (size_t)m * Kp + kb + kk;
-      if constexpr (MODE == 0) {
-        const float g = a.gpre[r * N + n];
-        const float* xs = sm + kk * S;
+  for (int j = 0; j < NPT; ++j)
 #pragma unroll
-        for (int l = 0; l < 32; ++l)
-          if (l < L) acc[l] += g * xs[l];
+    for (int l = 0; l < LL; ++l) acc[j][l] = 0.f;
+
+  for (int ch = c0; ch < c1; ++ch) {
+    const int m = ch / (Kp / FO_R), kb = (ch % (Kp / FO_R)) * FO_R;
+    __syncthreads();   // previous chunk fully consumed
+    // ---- stage source rows
+    for (int i = threadIdx.x; i < FO_R * cg; i += 256) {
+      const int rr = i / cg, c8 = i % cg, k = kb + rr;
+      const size_t r = (size_t)m * Kp + k;
+      float v[4][8];
+      if (k < K) {
+        if constexpr (MODE == 0) {
+          const float4 g0 = *reinterpret_cast<const float4*>(a.gpre + r * N + c8 * 8);
+          const float4 g1 = *reinterpret_cast<const float4*>(a.gpre + r * N + c8 * 8 + 4);
+          v[0][0] = g0.x; v[0][1] = g0.y; v[0][2] = g0.z; v[0][3] = g0.w;
+          v[0][4] = g1.x; v[0][5] = g1.y; v[0][6] = g1.z; v[0][7] = g1.w;
+        } else {
+          float wv[8];
+          Vec8<T>::load(w + r * N + c8 * 8, wv);
+          for (int cc = 0; cc < C; ++cc) Vec8<T>::load(sc + r * (size_t)(C * N) + (size_t)cc * N + c8 * 8, v[cc]);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            if (a.mask_type == 1) {
+              float mx = -3.4e38f, den = 0.f;
+              for (int cc = 0; cc < C; ++cc) mx = fmaxf(mx, v[cc][e]);
+              for (int cc = 0; cc < C; ++cc) { v[cc][e] = __expf(v[cc][e] - mx); den += v[cc][e]; }
+              for (int cc = 0; cc < C; ++cc) v[cc][e] = wv[e] * v[cc][e] / den;
+            } else if (a.mask_type == 0) {
+              for (int cc = 0; cc < C; ++cc) v[cc][e] = wv[e] * (v[cc][e] > 0.f ? v[cc][e] : 0.f);
+            } else {
+              for (int cc = 0; cc < C; ++cc) v[cc][e] = wv[e] * v[cc][e];
+            }
+          }
+        }
       } else {
-        const float wv = ld1<T>(w + r * N + n);
-        float sv[4];
-        float mx = -3.4e38f, den = 0.f;
-        for (int cc = 0; cc < C; ++cc) {
-          sv[cc] = ld1<T>(sc + r * (size_t)(C * N) + (size_t)cc * N + n);
-          mx = fmaxf(mx, sv[cc]);
-        }
-        if (a.mask_type == 1) {
-          for (int cc = 0; cc < C; ++cc) { sv[cc] = __expf(sv[cc] - mx); den += sv[cc]; }
-          for (int cc = 0; cc < C; ++cc) sv[cc] /= den;
-        } else if (a.mask_type == 0) {
-          for (int cc = 0; cc < C; ++cc) sv[cc] = sv[cc] > 0.f ? sv[cc] : 0.f;
-        }
-        for (int cc = 0; cc < C; ++cc) {
-          const float src = wv * sv[cc];
-          const float* gs = sm + cc * span + kk * S;
+        for (int cc = 0; cc < C; ++cc)
 #pragma unroll
-          for (int l = 0; l < 32; ++l)
-            if (l < L) acc[l] += src * gs[l];
-        }
+          for (int e = 0; e < 8; ++e) v[cc][e] = 0.f;
+      }
+      for (int cc = 0; cc < C; ++cc) {
+        float* d = srcs + (rr * C + cc) * N + c8 * 8;
+        *reinterpret_cast<float4*>(d) = make_float4(v[cc][0], v[cc][1], v[cc][2], v[cc][3]);
+        *reinterpret_cast<float4*>(d + 4) = make_float4(v[cc][4], v[cc][5], v[cc][6], v[cc][7]);
       }
     }
-    // mode 0 -> [N][L] (encoder weight [N,1,L]); mode 1 -> [L][N] (Linear(N, L) weight)
+    // ---- stage the signal span of every speaker
+    for (int i = threadIdx.x; i < C * span; i += 256) {
+      const int cc = i / span, j = i % span;
+      const long t = (long)kb * S + j;
+      float v = 0.f;
+      if (MODE == 0) v = t < a.T ? a.mixture[(size_t)m * a.T + t] : 0.f;
+      else v = t < a.T ? a.gest[((size_t)m * a.C + cc) * a.T + t] : 0.f;
+      sig[i] = v;
+    }
+    __syncthreads();
+    // ---- accumulate: thread owns channels n = tid + 256*j
 #pragma unroll
-    for (int l = 0; l < 32; ++l)
-      if (l < L) out[MODE == 0 ? (size_t)n * L + l : (size_t)l * N + n] = acc[l];
+    for (int j = 0; j < NPT; ++j) {
+      const int n = threadIdx.x + 256 * j;
+      if (n >= N) break;
+      for (int rr = 0; rr < FO_R; ++rr)
+        for (int cc = 0; cc < C; ++cc) {
+          const float sv = srcs[(rr * C + cc) * N + n];
+          const float* gs = sig + cc * span + rr * S;
+#pragma unroll
+          for (int l = 0; l < LL; ++l)
+            if (LT || l < L) acc[j][l] += sv * gs[l];
+        }
+    }
+  }
+  // mode 0 -> [N][L] (encoder weight [N,1,L]); mode 1 -> [L][N] (Linear(N, L) weight)
+  float* out = a.col_slab + (size_t)blockIdx.x * N * L;
+#pragma unroll
+  for (int j = 0; j < NPT; ++j) {
+    const int n = threadIdx.x + 256 * j;
+    if (n >= N) break;
+#pragma unroll
+    for (int l = 0; l < LL; ++l)
+      if (LT || l < L) out[MODE == 0 ? (size_t)n * L + l : (size_t)l * N + n] = acc[j][l];
   }
 }
 
@@ -405,29 +445,26 @@ hipError_t launch_enc_bwd_rows(DType dt, const CodecArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-int frame_outer_rows_per_chunk(const CodecArgs& a) {
-  // 256 frames per workgroup: M * Kp / 256 workgroups (400 at the paper batch)
-  const int r = 256;
-  return r < a.Kp ? r : a.Kp;
-}
 int frame_outer_chunks(const CodecArgs& a) {
-  const int rpc = frame_outer_rows_per_chunk(a);
-  return a.M * ((a.Kp + rpc - 1) / rpc);
+  const int n = a.M * (a.Kp / FO_R);
+  return n < FO_WGS ? n : FO_WGS;
 }
 
 hipError_t launch_frame_outer(DType dt, int mode, const CodecArgs& a, hipStream_t s) {
-  if (!codec_ok(a)) return hipErrorInvalidValue;
-  const int rpc = frame_outer_rows_per_chunk(a);
+  if (!codec_ok(a) || a.Kp % FO_R || a.N > 512 || a.L > FO_LMAX || a.C > 4) return hipErrorInvalidValue;
   const int C = mode == 0 ? 1 : a.C;
-  const size_t lds = (size_t)C * (rpc * a.S + a.L) * sizeof(float);
+  const size_t lds = ((size_t)FO_R * C * a.N + (size_t)C * (FO_R * a.S + a.L)) * sizeof(float);
   const dim3 g(frame_outer_chunks(a)), b(256);
+#define CTN_FO(T_, M_)                                                                             \
+  if (a.L == 20) hipLaunchKernelGGL((frame_outer_kernel<T_, M_, 20>), g, b, lds, s, a);            \
+  else if (a.L == 16) hipLaunchKernelGGL((frame_outer_kernel<T_, M_, 16>), g, b, lds, s, a);       \
+  else hipLaunchKernelGGL((frame_outer_kernel<T_, M_, 0>), g, b, lds, s, a);
   if (mode == 0) {
-    if (dt == BF16) hipLaunchKernelGGL((frame_outer_kernel<bf16raw, 0>), g, b, lds, s, a, rpc);
-    else hipLaunchKernelGGL((frame_outer_kernel<float, 0>), g, b, lds, s, a, rpc);
+    if (dt == BF16) { CTN_FO(bf16raw, 0) } else { CTN_FO(float, 0) }
   } else {
-    if (dt == BF16) hipLaunchKernelGGL((frame_outer_kernel<bf16raw, 1>), g, b, lds, s, a, rpc);
-    else hipLaunchKernelGGL((frame_outer_kernel<float, 1>), g, b, lds, s, a, rpc);
+    if (dt == BF16) { CTN_FO(bf16raw, 1) } else { CTN_FO(float, 1) }
   }
+#undef CTN_FO
   return hipGetLastError();
 }
 

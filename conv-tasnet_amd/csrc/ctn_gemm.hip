@@ -14,6 +14,8 @@
 // -> v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 accumulate).
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "ctn_common.h"
 #include "ctn_kernels.h"
 
@@ -465,8 +467,10 @@ __global__ __launch_bounds__(256) void gemm_cols_kernel(GemmCols p) {
   const bool pin = p0 + cc0 * E < p.P, qin = q0 + cc0 * E < p.Q;
 
   // Two register sets, each one k-step of both operands, loaded two steps ahead;
-  // rows past the chunk end are clamped to its last step (never stored).
-  struct Set { v4u a[NCH], b[NCH]; float2 sa[NCH], sb[NCH]; };
+  // rows past the chunk end are clamped to its last step (never stored).  A k-step
+  // never straddles utterances (Kp % CKR == 0): one gLN statistic per step.
+  constexpr int NST = NK == NORM_GLN ? 1 : NCH;
+  struct Set { v4u a[NCH], b[NCH]; f32x2_t sa[NST], sb[NST]; };
   auto gload = [&](Set& R, int ks) __attribute__((always_inline)) {
     const int r0 = rbeg + (ks < nks ? ks : nks - 1) * CKR;
 #pragma unroll
@@ -476,23 +480,64 @@ __global__ __launch_bounds__(256) void gemm_cols_kernel(GemmCols p) {
       // unconditional loads (clamped column; zeroed in swrite) keep the loop branch-free
       R.a[i] = ldg16(A + (size_t)r * p.lda + (pin ? p0 + cc0 * E : 0));
       R.b[i] = ldg16(B + (size_t)r * p.ldb + (qin ? q0 + cc0 * E : 0));
-      if constexpr (OPA != OP_PLAIN) R.sa[i] = p.aop.stats[stat_index<NK>(r, Kp)];
-      if constexpr (OPB != OP_PLAIN) R.sb[i] = p.bop.stats[stat_index<NK>(r, Kp)];
+      if constexpr (NK == NORM_CLN) {
+        if constexpr (OPA != OP_PLAIN) R.sa[i] = *reinterpret_cast<const f32x2_t*>(p.aop.stats + r);
+        if constexpr (OPB != OP_PLAIN) R.sb[i] = *reinterpret_cast<const f32x2_t*>(p.bop.stats + r);
+      }
+    }
+    if constexpr (NK == NORM_GLN) {
+      // indexed through the lane's own row so the load stays a (prefetched) vector
+      // load: a uniform index becomes an s_load the compiler sinks to its use
+      const int m = (r0 + tid / CPR) / Kp;
+      if constexpr (OPA != OP_PLAIN) R.sa[0] = *reinterpret_cast<const f32x2_t*>(p.aop.stats + m);
+      if constexpr (OPB != OP_PLAIN) R.sb[0] = *reinterpret_cast<const f32x2_t*>(p.bop.stats + m);
     }
   };
-  auto swrite = [&](const Set& R, int ks, char* st) __attribute__((always_inline)) {
+  // op(v) = PReLU?(v) * (rstd*gamma) + (beta - mean*rstd*gamma), packed
+  auto xform = [&](auto le1, v4u v, f32x2_t st, const float* g, const float* bt, float al, bool pr)
+      __attribute__((always_inline)) {
+    constexpr bool LE1 = decltype(le1)::value;
+    if constexpr (E == 8) {
+      float f[8];
+      unpack_bf16x8(v, f);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        f32x2_t x = {f[2 * e], f[2 * e + 1]};
+        if (pr) x = prelu2<LE1>(x, al);
+        const f32x2_t sc = f32x2_t{g[2 * e], g[2 * e + 1]} * st[1];
+        x = pfma(x, sc, pfma(sc, f32x2_t{-st[0], -st[0]}, f32x2_t{bt[2 * e], bt[2 * e + 1]}));
+        v[e] = pk_bf16(x[0], x[1]);
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float x = __uint_as_float(v[e]);
+        if (pr) x = LE1 ? fmaxf(x, al * x) : fminf(x, al * x);
+        v[e] = __float_as_uint((x - st[0]) * (st[1] * g[e]) + bt[e]);
+      }
+    }
+    return v;
+  };
+  auto swrite = [&](auto le1, const Set& R, int ks, char* st) __attribute__((always_inline)) {
     const int r0 = rbeg + ks * CKR;
+    const int k0 = r0 % Kp;   // frame of the step's first row (wave-uniform)
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int c = tid + 256 * i, rl = c / CPR;
-      const int r = r0 + rl;
-      const bool ok = r % Kp < K;   // padded frames contribute nothing
       v4u va = R.a[i], vb = R.b[i];
-      if constexpr (OPA != OP_PLAIN) va = apply_op_v<T, OPA>(va, R.sa[i], ga_, ba_, ala);
-      if constexpr (OPB != OP_PLAIN) vb = apply_op_v<T, OPB>(vb, R.sb[i], gb_, bb_, alb);
       const v4u z = v4u{0u, 0u, 0u, 0u};
-      va = ok && pin ? va : z;
-      vb = ok && qin ? vb : z;
+      // Transformed operands of padded frames would be beta, not 0: zero those rows,
+      // unless the other operand is plain (zero there) and the statistic is the
+      // utterance's (finite), so the product already vanishes.  Columns past P/Q hold
+      // clamped real data and only reach outputs the epilogue does not store.
+      if constexpr (OPA != OP_PLAIN) {
+        va = xform(le1, va, R.sa[NST == 1 ? 0 : i], ga_, ba_, ala, OPA == OP_PRELU_NORM);
+        if constexpr (!(OPB == OP_PLAIN && NK == NORM_GLN)) va = k0 + rl < K ? va : z;
+      }
+      if constexpr (OPB != OP_PLAIN) {
+        vb = xform(le1, vb, R.sb[NST == 1 ? 0 : i], gb_, bb_, alb, OPB == OP_PRELU_NORM);
+        if constexpr (!(OPA == OP_PLAIN && NK == NORM_GLN)) vb = k0 + rl < K ? vb : z;
+      }
       stg16(st + cswz<T>(rl, cc0 * E), va);
       stg16(st + CKR * PITCH + cswz<T>(rl, cc0 * E), vb);
     }
@@ -553,29 +598,40 @@ __global__ __launch_bounds__(256) void gemm_cols_kernel(GemmCols p) {
     }
   };
 
-  // Pipeline: step ks is written into LDS buffer ks&1 from register set ks&1 (loaded
-  // two steps earlier), then that set reloads step ks+2; one LDS-only barrier per
-  // step (the other buffer was last read before the previous barrier).
-  if (nks > 0) {
-    Set R0, R1;
-    gload(R0, 0);
-    gload(R1, 1);
+  // Pipeline: a ring of NSET register sets, each one k-step of both operands loaded
+  // NSET steps ahead; step ks is written into LDS buffer ks&1, its set reloads step
+  // ks+NSET, then one LDS-only barrier (the other buffer was last read before the
+  // previous barrier).  The loop is unrolled by NSET so every set index is static.
+  // Rows of padded frames are zero in the plain operands of this path, so they add
+  // nothing; transformed operands are zeroed there explicitly.
+  constexpr int NSET = 2;   // deeper rings measured slower (register pressure)
+  auto run = [&](auto le1) __attribute__((always_inline)) {
+    Set R[NSET];
+#pragma unroll
+    for (int u = 0; u < NSET; ++u) gload(R[u], u);
     int ks = 0;
-    for (; ks + 1 < nks; ks += 2) {   // full pairs: the same loads trail every wait
-      swrite(R0, ks, smem);
-      gload(R0, ks + 2);
-      lds_barrier();
-      compute(smem);
-      swrite(R1, ks + 1, smem + STAGE);
-      gload(R1, ks + 3);
-      lds_barrier();
-      compute(smem + STAGE);
+    for (; ks + NSET - 1 < nks; ks += NSET) {   // full rounds: the same loads trail every wait
+#pragma unroll
+      for (int u = 0; u < NSET; ++u) {
+        swrite(le1, R[u], ks + u, smem + (u & 1) * STAGE);
+        gload(R[u], ks + u + NSET);
+        lds_barrier();
+        compute(smem + (u & 1) * STAGE);
+      }
     }
-    if (ks < nks) {   // odd tail
-      swrite(R0, ks, smem);
-      lds_barrier();
-      compute(smem);
+#pragma unroll
+    for (int u = 0; u < NSET; ++u) {   // tail (ks is a multiple of NSET, so parity = u & 1)
+      if (ks + u < nks) {
+        swrite(le1, R[u], ks + u, smem + (u & 1) * STAGE);
+        lds_barrier();
+        compute(smem + (u & 1) * STAGE);
+      }
     }
+  };
+  if (nks > 0) {
+    constexpr bool PR = OPA == OP_PRELU_NORM || OPB == OP_PRELU_NORM;
+    if (!PR || (OPB == OP_PRELU_NORM ? alb : ala) <= 1.f) run(std::true_type{});
+    else run(std::false_type{});
   }
   // lane holds D[p = p0 + wp*64 + i*16 + lg*4 + q][q = q0 + wq*64 + j*16 + lr]
   float* Cp = p.Cpart + (size_t)chunk * p.P * p.Q;
