@@ -190,7 +190,9 @@ TbLayout tb_layout(const ctn_tblock_desc* d, int backward, void* ws) {
   L.parts1 = gemm_rows_tiles_per_group(dtl, g1);
   DwArgs da{};
   da.g = rg; da.H = d->H; da.P = d->P; da.norm = d->norm_type; da.dil = d->dilation; da.pad = tb_pad(d);
-  L.parts2 = dw_parts_per_group(da);
+  da.seg = dw_seg(da, false);
+  L.parts2 = dw_parts_per_group(da);   // forward comb geometry (norm-2 statistics)
+  da.seg = dw_seg(da, true);            // backward comb geometry from here on
   if (!backward) {
     if (d->dtype == CTN_DTYPE_BF16) {
       L.w1s = c.take<void>((size_t)d->H * d->B * es);
@@ -206,7 +208,7 @@ TbLayout tb_layout(const ctn_tblock_desc* d, int backward, void* ws) {
     GemmRows ga = tb_gemmA(d);
     L.partsA = gemm_rows_tiles_per_group(dtl, ga);
     L.slabA = c.take<double2>((size_t)G * L.partsA * sizeof(double2));
-    L.partsD = L.parts2;
+    L.partsD = dw_parts_per_group(da);
     L.slabD = c.take<double2>((size_t)G * L.partsD * sizeof(double2));
     L.colD = c.take<float>((size_t)dw_blocks(da) * dw_col_stride(da) * sizeof(float));
     L.alphaSlab = c.take<float>((size_t)ew_blocks(da) * sizeof(float));
@@ -277,6 +279,7 @@ extern "C" int ctn_tblock_forward(const ctn_tblock_desc* d, const ctn_tblock_par
   // norm1 apply + depthwise dilated conv, PReLU statistics for norm2
   DwArgs da{};
   da.g = rg; da.H = d->H; da.P = d->P; da.dil = d->dilation; da.pad = tb_pad(d); da.norm = d->norm_type;
+  da.seg = dw_seg(da, false);
   da.h1 = sv->h1; da.st1 = st1;
   da.alpha1 = p->alpha1; da.gamma1 = p->gamma1; da.beta1 = p->beta1; da.alpha2 = p->alpha2;
   da.wd = p->wd; da.d_out = sv->d; da.slab2 = L.slab2;
@@ -348,6 +351,7 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
   //     wd, gamma2/beta2, alpha2)
   DwArgs da{};
   da.g = rg; da.H = d->H; da.P = d->P; da.dil = d->dilation; da.pad = tb_pad(d); da.norm = d->norm_type;
+  da.seg = dw_seg(da, true);
   da.h1 = sv->h1; da.d = sv->d; da.st1 = st1; da.st2 = st2;
   da.alpha1 = p->alpha1; da.gamma1 = p->gamma1; da.beta1 = p->beta1; da.alpha2 = p->alpha2; da.gamma2 = p->gamma2;
   da.wd = p->wd;

@@ -107,6 +107,7 @@ struct DwArgs {
   Rows g;
   int H, P, dil, pad;
   int norm;                              // NormKind of both block norms
+  int seg;                               // comb steps per work item (dw_seg)
   const void* h1;                        // pre-PReLU output of the block's first 1x1 conv
   const void* d;                         // pre-PReLU output of the depthwise conv (bwd)
   const float2* st1; const float2* st2;  // forward (mean, rstd)
@@ -126,7 +127,8 @@ struct DwArgs {
   void* gh1_out;                         // (ew) dL/dh1
   float* alpha_slab;                     // (ew) [blocks] galpha1 partials
 };
-int dw_blocks(const DwArgs& a);        // depthwise (comb) kernels
+int dw_seg(const DwArgs& a, bool bwd);   // comb segment length sizing one resident round
+int dw_blocks(const DwArgs& a);        // depthwise (comb) kernels (a.seg set)
 int ew_blocks(const DwArgs& a);        // norm1_bwd (128-row blocks)
 int dw_parts_per_group(const DwArgs& a);   // slab parts per utterance (gLN) or per row (cLN)
 __host__ __device__ int dw_col_stride(const DwArgs& a);

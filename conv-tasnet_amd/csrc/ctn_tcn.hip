@@ -20,12 +20,13 @@ namespace ctn {
 
 constexpr int DW_RPB = 128;   // rows per workgroup (element-wise kernels)
 constexpr int DW_MAXP = 8;
-constexpr int DW_SEG = 32;    // comb steps per work item (depthwise kernels)
+constexpr int DW_MINSEG = 16; // shortest comb segment (halo rows cost (P-1)/seg)
+constexpr int DW_WPS_FWD = 4, DW_WPS_BWD = 2;   // waves/SIMD the kernels' VGPR budgets allow
 
 // ---------------------------------------------------------------------------
 // Comb decomposition of the dilated depthwise conv.  Rows of one utterance are
 // split into residue classes rho mod d; a work item walks rows rho + j*d for
-// j in one DW_SEG-long segment.  A lane group of H/8 lanes owns one item and
+// j in one segment of a.seg steps (dw_seg).  A lane group of H/8 lanes owns one item and
 // all H channels of its rows (8 per lane, 16-byte vectors); the P taps of a
 // row are consecutive comb steps, so they live in a sliding register window:
 // every row is loaded and transformed once (plus P-1 halo rows per segment)
@@ -39,12 +40,34 @@ __host__ __device__ inline CombGeom comb_geom(const DwArgs& a) {
   g.cg = a.H / 8;
   g.ipw = 4 * (64 / g.cg);
   g.jmax = (a.g.Kp + a.dil - 1) / a.dil;
-  g.nseg = (g.jmax + DW_SEG - 1) / DW_SEG;
+  g.nseg = (g.jmax + a.seg - 1) / a.seg;
   g.items = a.dil * g.nseg;
   g.wgpu = (g.items + g.ipw - 1) / g.ipw;
   return g;
 }
 
+// Segment length such that all work items of the launch are resident at once:
+// a wave owns 64/(H/8) items and walks its segment serially, so a second, partly
+// filled round of waves would cost a whole segment time.  Items per utterance are
+// dil * ceil(jmax/seg); when dil alone exceeds the budget the segment is the
+// whole residue class (jmax steps, the shortest possible).
+int dw_seg(const DwArgs& a, bool bwd) {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    return n;
+  }();
+  const long cap = (long)cus * 4 * (bwd ? DW_WPS_BWD : DW_WPS_FWD) * (64 / (a.H / 8));
+  const long per_utt = cap / (a.g.M > 0 ? a.g.M : 1);
+  const int jmax = (a.g.Kp + a.dil - 1) / a.dil;
+  long nseg = per_utt / a.dil;
+  if (nseg < 1) nseg = 1;
+  int seg = (int)((jmax + nseg - 1) / nseg);
+  if (seg < DW_MINSEG) seg = DW_MINSEG;
+  return seg;
+}
 int dw_blocks(const DwArgs& a) { return a.g.M * comb_geom(a).wgpu; }
 int dw_parts_per_group(const DwArgs& a) { return a.norm == NORM_GLN ? comb_geom(a).wgpu : 1; }
 int ew_blocks(const DwArgs& a) { return (int)(a.g.rows() / DW_RPB); }
@@ -84,8 +107,8 @@ CTN_DEV CombItem comb_item(const DwArgs& a, const CombGeom& gm) {
   const int id = it.wgi * gm.ipw + wv * (64 / gm.cg) + it.sub;
   it.active = id < gm.items;
   it.rho = it.active ? id / gm.nseg : 0;
-  it.j0 = it.active ? (id % gm.nseg) * DW_SEG : 0;
-  it.j1 = it.j0 + DW_SEG < gm.jmax ? it.j0 + DW_SEG : gm.jmax;
+  it.j0 = it.active ? (id % gm.nseg) * a.seg : 0;
+  it.j1 = it.j0 + a.seg < gm.jmax ? it.j0 + a.seg : gm.jmax;
   if (!it.active) it.j1 = it.j0;
   it.base = it.m * a.g.Kp;
   return it;
@@ -406,7 +429,7 @@ __global__ __launch_bounds__(256) void norm1_bwd_kernel(DwArgs a) {
 static hipError_t dw_check(const DwArgs& a) {
   const int cg = a.H / 8;
   if (a.H % 8 != 0 || cg > 64 || (cg & (cg - 1)) || a.P < 1 || a.P > DW_MAXP || a.g.Kp % DW_RPB != 0 ||
-      a.dil < 1)
+      a.dil < 1 || a.seg < 1)
     return hipErrorInvalidValue;
   const int pown = a.pad / a.dil;
   if (pown * a.dil != a.pad || (pown != a.P - 1 && pown != (a.P - 1) / 2)) return hipErrorInvalidValue;
