@@ -110,6 +110,7 @@ def main():
 
     import conv_tasnet as ct
     import ctn_lib as L
+    import ctn_optim
     import pit_criterion as pc
     import synthetic
 
@@ -123,7 +124,9 @@ def main():
     model.act_dtype = torch.float32 if args.fp32 else torch.bfloat16
     if world > 1:
         model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], bucket_cap_mb=25)
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
+    # the solver's update (src/solver.py:184-186) on the HIP path: one launch for
+    # the clip norm, one for the clip scale, one for Adam over all 294 tensors
+    opt = ctn_optim.Adam(model.parameters(), lr=1e-3)
     mix, src = synthetic.speech_like(M, C, T, 1234 + rank)
     mix, src = mix.to(dev), src.to(dev)
     lens = torch.full((M,), T, dtype=torch.int64, device=dev)
@@ -133,7 +136,7 @@ def main():
         loss = pc.cal_loss(src, est, lens)[0]
         opt.zero_grad(set_to_none=True)
         loss.backward()
-        torch.nn.utils.clip_grad_norm_(model.parameters(), 5.0)
+        ctn_optim.clip_grad_norm_(model.parameters(), 5.0)
         opt.step()
         return loss
 

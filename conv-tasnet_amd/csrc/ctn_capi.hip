@@ -1,6 +1,7 @@
 // extern "C" entry points of libctn_hip.so (include/ctn.h) and the native
 // launch sequences behind them.  Each entry validates its descriptor, carves
 // the caller's workspace, and enqueues its kernels on the caller's stream.
+#include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
@@ -723,5 +724,55 @@ extern "C" int ctn_pit_backward(const ctn_pit_desc* d, const float* source, cons
   a.src = source; a.est = est; a.lengths = lengths; a.coef = const_cast<float*>(coef);
   a.g_loss = g_loss; a.g_maxsnr = g_max_snr; a.gest = g_est;
   CTN_HIP(launch_pit_backward(a, (hipStream_t)stream));
+  return CTN_OK;
+}
+
+// ===========================================================================
+// Parameter update (clip_grad_norm_ + Adam), ctn_optim.hip
+// ===========================================================================
+static_assert(sizeof(ctn_opt_segment) == sizeof(OptSegment), "segment layout");
+static_assert(sizeof(ctn_opt_chunk) == sizeof(OptChunk), "chunk layout");
+
+extern "C" int ctn_opt_plan(const ctn_opt_segment* segs, int nseg, ctn_opt_chunk* chunks, int max_chunks) {
+  if (!segs || nseg < 0) return -fail(CTN_ERR_ARG, "ctn_opt_plan: bad segment table");
+  long total = 0;
+  for (int i = 0; i < nseg; ++i) {
+    const ctn_opt_segment& g = segs[i];
+    if (g.numel < 0 || !g.grad) return -fail(CTN_ERR_ARG, "ctn_opt_plan: segment %d has no grad or numel < 0", i);
+    const uintptr_t ptrs[4] = {(uintptr_t)g.param, (uintptr_t)g.grad, (uintptr_t)g.exp_avg, (uintptr_t)g.exp_avg_sq};
+    bool aligned = true;
+    for (uintptr_t q : ptrs) aligned = aligned && (q % 16 == 0);
+    for (int64_t off = 0; off < g.numel; off += OPT_CHUNK) {
+      const int64_t len = g.numel - off < OPT_CHUNK ? g.numel - off : OPT_CHUNK;
+      if (chunks && total < max_chunks)
+        chunks[total] = ctn_opt_chunk{i, (uint32_t)len | (aligned ? 0u : OPT_UNALIGNED), off};
+      ++total;
+    }
+  }
+  if (total > INT32_MAX) return -fail(CTN_ERR_ARG, "ctn_opt_plan: too many chunks");
+  return (int)total;
+}
+
+extern "C" int ctn_grad_clip_norm(const ctn_opt_segment* segs, const ctn_opt_chunk* chunks, int nchunks,
+                                  float max_norm, float* total_norm, float* partial, void* stream) {
+  if (!segs || !chunks || !partial || nchunks < 0) return fail(CTN_ERR_ARG, "ctn_grad_clip_norm: null table");
+  const hipStream_t s = (hipStream_t)stream;
+  const OptSegment* sg = reinterpret_cast<const OptSegment*>(segs);
+  const OptChunk* ch = reinterpret_cast<const OptChunk*>(chunks);
+  CTN_HIP(launch_grad_sqnorm(sg, ch, nchunks, partial, s));
+  CTN_HIP(launch_grad_clip(sg, ch, nchunks, partial, max_norm, total_norm, s));
+  return CTN_OK;
+}
+
+extern "C" int ctn_adam_step(const ctn_opt_segment* segs, const ctn_opt_chunk* chunks, int nchunks,
+                             const ctn_adam_hparams* hp, void* stream) {
+  if (!segs || !chunks || !hp || nchunks < 0 || hp->step < 1)
+    return fail(CTN_ERR_ARG, "ctn_adam_step: bad arguments");
+  // bias corrections in double on the host, as torch.optim.Adam computes them
+  const double bc1 = 1.0 - pow((double)hp->beta1, (double)hp->step);
+  const double bc2 = 1.0 - pow((double)hp->beta2, (double)hp->step);
+  AdamArgs a{hp->beta1, hp->beta2, hp->eps, hp->weight_decay, (float)(hp->lr / bc1), (float)sqrt(bc2)};
+  CTN_HIP(launch_adam(reinterpret_cast<const OptSegment*>(segs), reinterpret_cast<const OptChunk*>(chunks), nchunks,
+                      a, (hipStream_t)stream));
   return CTN_OK;
 }

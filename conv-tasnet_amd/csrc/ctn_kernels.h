@@ -136,4 +136,21 @@ hipError_t launch_dw_fwd(DType dt, const DwArgs& a, hipStream_t s);
 hipError_t launch_dw_bwd(DType dt, const DwArgs& a, hipStream_t s);
 hipError_t launch_norm1_bwd(DType dt, const DwArgs& a, hipStream_t s);
 
+// ---------------------------------------------------------------------------
+// parameter update (ctn_optim.hip); layouts identical to ctn_opt_segment /
+// ctn_opt_chunk of include/ctn.h
+// ---------------------------------------------------------------------------
+struct OptSegment { float* p; float* g; float* m; float* v; int64_t n; };
+struct OptChunk { int32_t seg; uint32_t len; int64_t off; };
+constexpr int OPT_CHUNK = 8192;                 // elements per workgroup
+constexpr uint32_t OPT_UNALIGNED = 0x80000000u;  // len flag: scalar path
+constexpr uint32_t OPT_LEN_MASK = 0x7fffffffu;
+struct AdamArgs { float b1, b2, eps, wd, step_size, bc2_sqrt; };
+hipError_t launch_grad_sqnorm(const OptSegment* segs, const OptChunk* chunks, int nchunks, float* partial,
+                              hipStream_t s);
+hipError_t launch_grad_clip(const OptSegment* segs, const OptChunk* chunks, int nchunks, const float* partial,
+                            float max_norm, float* total_norm, hipStream_t s);
+hipError_t launch_adam(const OptSegment* segs, const OptChunk* chunks, int nchunks, const AdamArgs& a,
+                       hipStream_t s);
+
 }  // namespace ctn

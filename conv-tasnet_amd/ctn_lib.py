@@ -62,6 +62,20 @@ class PitDesc(ctypes.Structure):
 MASK_IDENTITY = 2
 
 
+class OptSegment(ctypes.Structure):
+    _fields_ = [("param", c_void_p), ("grad", c_void_p), ("exp_avg", c_void_p), ("exp_avg_sq", c_void_p),
+                ("numel", ctypes.c_int64)]
+
+
+class OptChunk(ctypes.Structure):
+    _fields_ = [("seg", c_int32), ("len", ctypes.c_uint32), ("off", ctypes.c_int64)]
+
+
+class AdamHParams(ctypes.Structure):
+    _fields_ = [("lr", ctypes.c_float), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float),
+                ("eps", ctypes.c_float), ("weight_decay", ctypes.c_float), ("step", c_int32)]
+
+
 # ----------------------------------------------------------------------------
 _lib = None
 _lock = threading.Lock()
@@ -85,6 +99,10 @@ _SIGS = {
     "ctn_pit_workspace_bytes": (c_size_t, [c_void_p]),
     "ctn_pit_forward": (ctypes.c_int, [c_void_p] + [c_void_p] * 8 + [c_void_p, c_size_t, c_void_p]),
     "ctn_pit_backward": (ctypes.c_int, [c_void_p] + [c_void_p] * 7 + [c_void_p]),
+    "ctn_opt_plan": (ctypes.c_int, [c_void_p, ctypes.c_int, c_void_p, ctypes.c_int]),
+    "ctn_grad_clip_norm": (ctypes.c_int, [c_void_p, c_void_p, ctypes.c_int, ctypes.c_float, c_void_p, c_void_p,
+                                          c_void_p]),
+    "ctn_adam_step": (ctypes.c_int, [c_void_p, c_void_p, ctypes.c_int, c_void_p, c_void_p]),
     "ctn_timer_enable": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "ctn_timer_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
 }

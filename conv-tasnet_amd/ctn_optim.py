@@ -1,0 +1,198 @@
+"""Parameter update of the training step on the HIP path.
+
+Drop-ins for the two calls the reference solver makes after backward
+(src/solver.py:184-186), each one kernel launch over ALL parameter tensors
+instead of one per tensor (or per ~100 tensors):
+
+    torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm)   ->  clip_grad_norm_
+    torch.optim.Adam(model.parameters(), lr, weight_decay=l2)      ->  Adam
+                                                     (built at src/train.py:129-133)
+
+Same arguments, same in-place effects and the same ``state_dict`` layout as the
+torch versions (per parameter ``step`` / ``exp_avg`` / ``exp_avg_sq``), so
+reference checkpoints' ``optim_dict`` load into this optimizer and back.
+Only fp32, dense, contiguous ROCm-device tensors are accepted; anything else
+raises ``CtnLibraryError`` (there is no fallback).
+"""
+from __future__ import annotations
+
+import ctypes
+from collections import OrderedDict
+
+import torch
+
+import ctn_lib as L
+
+_PLAN_CACHE_MAX = 8
+
+
+class _Plan:
+    """Device chunk table for one list of tensor sizes (and 16-byte alignments).
+
+    Chunks depend only on sizes and alignment, so the plan survives the
+    gradient tensors being reallocated every step (``zero_grad(set_to_none=
+    True)``); the segment table of pointers is uploaded per call instead
+    (``upload_segments``), asynchronously from pinned memory."""
+
+    def __init__(self, segs: list, device):
+        lib = L.load()
+        arr = (L.OptSegment * len(segs))(*segs)
+        n = lib.ctn_opt_plan(arr, len(segs), None, 0)
+        if n < 0:
+            L.check(-n, "ctn_opt_plan")
+        chunks = (L.OptChunk * max(n, 1))()
+        L.check(0 if lib.ctn_opt_plan(arr, len(segs), chunks, n) == n else 1, "ctn_opt_plan")
+        self.nchunks = n
+        self.nseg = len(segs)
+        self.chunks = torch.frombuffer(bytearray(bytes(chunks)), dtype=torch.uint8).to(device)
+        self.partial = torch.empty(max(n, 1), dtype=torch.float32, device=device)
+        self.device = device
+
+
+def upload_segments(segs: list, device) -> torch.Tensor:
+    """Segment table -> device, async: torch's pinned-host caching allocator keeps
+    the staging block alive until the copy has run, so no later call can
+    overwrite it while the CPU runs ahead of the GPU."""
+    arr = (L.OptSegment * len(segs))(*segs)
+    host = torch.empty(ctypes.sizeof(arr), dtype=torch.uint8, pin_memory=True)
+    ctypes.memmove(host.data_ptr(), ctypes.addressof(arr), ctypes.sizeof(arr))
+    return host.to(device, non_blocking=True)
+
+
+def _aligned(*ts) -> bool:
+    return all(t is None or t.data_ptr() % 16 == 0 for t in ts)
+
+
+def _cached_plan(cache: OrderedDict, key, build):
+    plan = cache.get(key)
+    if plan is None:
+        plan = build()
+        cache[key] = plan
+        while len(cache) > _PLAN_CACHE_MAX:
+            cache.popitem(last=False)
+    else:
+        cache.move_to_end(key)
+    return plan
+
+
+def _check_tensor(t: torch.Tensor, what: str):
+    L.require_device(t, what)
+    if t.dtype != torch.float32 or t.is_sparse or not t.is_contiguous():
+        raise L.CtnLibraryError(f"{what}: needs dense contiguous float32 tensors (got {t.dtype}, "
+                                f"contiguous={t.is_contiguous()})")
+
+
+_clip_plans: OrderedDict = OrderedDict()
+
+
+@torch.no_grad()
+def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0, error_if_nonfinite: bool = False,
+                    foreach=None) -> torch.Tensor:
+    """torch.nn.utils.clip_grad_norm_ (2-norm): grads *= min(1, max_norm / (norm + 1e-6)).
+
+    Returns the total norm of all gradients as a 0-dim device tensor."""
+    if isinstance(parameters, torch.Tensor):
+        parameters = [parameters]
+    grads = [p.grad for p in parameters if p.grad is not None]
+    if not grads:
+        return torch.tensor(0.0)
+    if float(norm_type) != 2.0:
+        raise L.CtnLibraryError(f"clip_grad_norm_: norm_type {norm_type} is not implemented (2.0 only)")
+    dev = grads[0].device
+    for g in grads:
+        _check_tensor(g, "clip_grad_norm_")
+        if g.device != dev:
+            raise L.CtnLibraryError("clip_grad_norm_: gradients on more than one device")
+    segs = [L.OptSegment(None, g.data_ptr(), None, None, g.numel()) for g in grads]
+    key = (dev, tuple((g.numel(), _aligned(g)) for g in grads))
+    plan = _cached_plan(_clip_plans, key, lambda: _Plan(segs, dev))
+    segs_dev = upload_segments(segs, dev)
+    total = torch.empty((), dtype=torch.float32, device=dev)
+    L.check(L.load().ctn_grad_clip_norm(segs_dev.data_ptr(), plan.chunks.data_ptr(), plan.nchunks,
+                                        float(max_norm), total.data_ptr(), plan.partial.data_ptr(),
+                                        L.stream_handle(dev)), "ctn_grad_clip_norm")
+    if error_if_nonfinite and not bool(torch.isfinite(total)):
+        raise RuntimeError(f"The total norm of order {float(norm_type)} for gradients from `parameters` "
+                           f"is non-finite, so it cannot be clipped.")
+    return total
+
+
+class Adam(torch.optim.Optimizer):
+    """torch.optim.Adam (amsgrad=False, maximize=False) as one HIP launch per step.
+
+    ``state[p]`` holds ``step`` (0-dim float32 CPU tensor, as torch's default
+    Adam), ``exp_avg`` and ``exp_avg_sq`` (device tensors shaped like ``p``)."""
+
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 0.0, amsgrad: bool = False, *, maximize: bool = False, **_ignored):
+        if amsgrad or maximize:
+            raise L.CtnLibraryError("Adam: amsgrad / maximize are not implemented on the HIP path")
+        if not 0.0 <= lr or not 0.0 <= eps or not 0.0 <= weight_decay:
+            raise ValueError("Adam: invalid lr / eps / weight_decay")
+        if not (0.0 <= betas[0] < 1.0 and 0.0 <= betas[1] < 1.0):
+            raise ValueError(f"Adam: invalid betas {betas}")
+        defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay, amsgrad=False,
+                        maximize=False, foreach=None, capturable=False, differentiable=False, fused=None)
+        super().__init__(params, defaults)
+        self._plans: OrderedDict = OrderedDict()
+        self._steps: dict = {}   # param -> int step (mirrored into state['step'] lazily)
+
+    # --- state_dict compatibility: keep state['step'] tensors current
+    def _sync_steps(self):
+        for p, n in self._steps.items():
+            st = self.state.get(p)
+            if st is not None:
+                st["step"] = torch.tensor(float(n))
+
+    def state_dict(self):
+        self._sync_steps()
+        return super().state_dict()
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        self._steps = {}
+        for group in self.param_groups:
+            for p in group["params"]:
+                st = self.state.get(p)
+                if st and "step" in st:
+                    self._steps[p] = int(float(st["step"]))
+                    for k in ("exp_avg", "exp_avg_sq"):
+                        if k in st and (st[k].dtype != torch.float32 or not st[k].is_contiguous()):
+                            st[k] = st[k].float().contiguous()
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        lib = L.load()
+        for group in self.param_groups:
+            by_step: dict = {}
+            for p in group["params"]:
+                g = p.grad
+                if g is None:
+                    continue
+                _check_tensor(p, "Adam")
+                _check_tensor(g, "Adam")
+                st = self.state[p]
+                if "exp_avg" not in st:
+                    st["step"] = torch.tensor(0.0)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                n = self._steps.get(p, int(float(st["step"]))) + 1
+                self._steps[p] = n
+                by_step.setdefault(n, []).append((p, g, st["exp_avg"], st["exp_avg_sq"]))
+            b1, b2 = group["betas"]
+            for n, items in by_step.items():
+                dev = items[0][0].device
+                segs = [L.OptSegment(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel())
+                        for p, g, m, v in items]
+                key = (dev, tuple((p.numel(), _aligned(p, g, m, v)) for p, g, m, v in items))
+                plan = _cached_plan(self._plans, key, lambda: _Plan(segs, dev))
+                segs_dev = upload_segments(segs, dev)
+                hp = L.AdamHParams(float(group["lr"]), float(b1), float(b2), float(group["eps"]),
+                                   float(group["weight_decay"]), n)
+                L.check(lib.ctn_adam_step(segs_dev.data_ptr(), plan.chunks.data_ptr(), plan.nchunks,
+                                          ctypes.byref(hp), L.stream_handle(dev)), "ctn_adam_step")
+        return loss

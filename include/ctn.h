@@ -143,6 +143,40 @@ int ctn_pit_backward(const ctn_pit_desc* d, const float* source, const float* es
                      const float* coef, const float* g_loss, const float* g_max_snr, float* g_est, void* stream);
 
 /* -------------------------------------------------------------------------
+ * Parameter update: replaces torch.nn.utils.clip_grad_norm_(params, max_norm)
+ * (src/solver.py:184-185) and torch.optim.Adam(params, lr, weight_decay=l2)
+ * (src/train.py:129-133, stepped at src/solver.py:186) with one launch each
+ * over ALL parameter tensors.  A segment describes one parameter tensor (fp32
+ * device pointers; exp_avg/exp_avg_sq may be NULL for clipping); the chunk
+ * table (ctn_opt_plan, host memory, copied to the device by the caller) cuts
+ * the segments into workgroup pieces.  Rebuild the plan whenever a pointer or
+ * size changes.
+ * ------------------------------------------------------------------------- */
+typedef struct {
+  float* param;
+  float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  int64_t numel;
+} ctn_opt_segment;
+typedef struct { int32_t seg; uint32_t len; int64_t off; } ctn_opt_chunk;
+typedef struct {
+  float lr, beta1, beta2, eps, weight_decay;
+  int32_t step;   /* 1-based step count after the increment (bias correction) */
+} ctn_adam_hparams;
+
+/* segs: host copy of the segment table.  Returns the number of chunks (writes
+ * up to max_chunks entries when chunks != NULL), or a negative ctn_status. */
+int ctn_opt_plan(const ctn_opt_segment* segs, int nseg, ctn_opt_chunk* chunks, int max_chunks);
+/* grads *= min(1, max_norm / (||grads||_2 + 1e-6)); *total_norm = ||grads||_2 (device).
+ * segs/chunks: device tables; partial: device scratch of nchunks floats. */
+int ctn_grad_clip_norm(const ctn_opt_segment* segs, const ctn_opt_chunk* chunks, int nchunks, float max_norm,
+                       float* total_norm, float* partial, void* stream);
+/* one Adam step of every segment (param, exp_avg, exp_avg_sq updated in place) */
+int ctn_adam_step(const ctn_opt_segment* segs, const ctn_opt_chunk* chunks, int nchunks, const ctn_adam_hparams* hp,
+                  void* stream);
+
+/* -------------------------------------------------------------------------
  * Opt-in kernel timer (bench.py roofline): when enabled, every launch of the
  * selected kernel family is bracketed by hipEvents on its stream.
  * kind: 0 off, 1 block-forward first 1x1 GEMM, 2 depthwise forward,
