@@ -276,7 +276,9 @@ extern "C" int ctn_tblock_forward(const ctn_tblock_desc* d, const ctn_tblock_par
     TimedScope ts(1, s);
     CTN_HIP(launch_gemm_rows(dt, g1, s));
   }
-  CTN_HIP(launch_stats_finalize(L.slab1, G, L.parts1, cnt, 0, (float)kEps, st1, s));
+  // gLN: the consumers finalize the statistics from the slab partials (StatFold)
+  const bool fold = d->norm_type == CTN_NORM_GLN;
+  if (!fold) CTN_HIP(launch_stats_finalize(L.slab1, G, L.parts1, cnt, 0, (float)kEps, st1, s));
   // norm1 apply + depthwise dilated conv, PReLU statistics for norm2
   DwArgs da{};
   da.g = rg; da.H = d->H; da.P = d->P; da.dil = d->dilation; da.pad = tb_pad(d); da.norm = d->norm_type;
@@ -284,11 +286,11 @@ extern "C" int ctn_tblock_forward(const ctn_tblock_desc* d, const ctn_tblock_par
   da.h1 = sv->h1; da.st1 = st1;
   da.alpha1 = p->alpha1; da.gamma1 = p->gamma1; da.beta1 = p->beta1; da.alpha2 = p->alpha2;
   da.wd = p->wd; da.d_out = sv->d; da.slab2 = L.slab2;
+  if (fold) da.f_st1 = gemm_rows_stat_fold(dt, g1, L.slab1, cnt, (float)kEps, 0, st1);
   {
     TimedScope ts(2, s);
     CTN_HIP(launch_dw_fwd(dt, da, s));
   }
-  CTN_HIP(launch_stats_finalize(L.slab2, G, L.parts2, cnt, 0, (float)kEps, st2, s));
   // norm2 apply (+PReLU) on the operand, 1x1 conv H->B, residual add
   GemmRows g2{};
   g2.g = rg; g2.Kred = d->H; g2.Nout = d->B; g2.norm = d->norm_type;
@@ -298,6 +300,8 @@ extern "C" int ctn_tblock_forward(const ctn_tblock_desc* d, const ctn_tblock_par
   g2.W = w2; g2.ldw = d->H;
   g2.epi = EPI_RESID; g2.R = x; g2.ldr = d->B;
   g2.C = y; g2.ldc = d->B;
+  if (fold && gemm_ws_can_fold(dt, g2)) g2.aop.fold = StatFold{L.slab2, L.parts2, cnt, (float)kEps, 0, st2};
+  else CTN_HIP(launch_stats_finalize(L.slab2, G, L.parts2, cnt, 0, (float)kEps, st2, s));
   CTN_HIP(launch_gemm_rows(dt, g2, s));
   return CTN_OK;
 }
@@ -338,7 +342,8 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
     TimedScope ts(3, s);
     CTN_HIP(launch_gemm_rows(dt, ga, s));
   }
-  CTN_HIP(launch_stats_finalize(L.slabA, G, L.partsA, cnt, 1, 0.f, L.sums2, s));
+  const bool fold = d->norm_type == CTN_NORM_GLN;   // gLN: consumers finalize the sums (StatFold)
+  if (!fold) CTN_HIP(launch_stats_finalize(L.slabA, G, L.partsA, cnt, 1, 0.f, L.sums2, s));
   // (b) dW2 = gy^T . norm2(PReLU(d))
   GemmCols c2{};
   c2.g = rg; c2.P = d->B; c2.Q = d->H;
@@ -357,11 +362,14 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
   da.alpha1 = p->alpha1; da.gamma1 = p->gamma1; da.beta1 = p->beta1; da.alpha2 = p->alpha2; da.gamma2 = p->gamma2;
   da.wd = p->wd;
   da.ga2 = L.G1; da.sm2 = L.sums2; da.ga1_out = L.G2; da.slab1 = L.slabD; da.col_slab = L.colD;
+  if (fold) da.f_sm2 = gemm_rows_stat_fold(dt, ga, L.slabA, cnt, 0.f, 1, nullptr);
   CTN_HIP(launch_dw_bwd(dt, da, s));
-  CTN_HIP(launch_stats_finalize(L.slabD, G, L.partsD, cnt, 1, 0.f, L.sums1, s));
+  if (!fold) CTN_HIP(launch_stats_finalize(L.slabD, G, L.partsD, cnt, 1, 0.f, L.sums1, s));
   // (d) norm1 backward finish + PReLU1 backward -> G1 = dL/dh1
   DwArgs de = da;
   de.ga2 = L.G2; de.sm1 = L.sums1; de.gh1_out = L.G1; de.alpha_slab = L.alphaSlab;
+  de.f_sm2 = StatFold{};
+  if (fold) de.f_sm1 = StatFold{L.slabD, L.partsD, cnt, 0.f, 1, nullptr};
   CTN_HIP(launch_norm1_bwd(dt, de, s));
   // (e) gx = gh1 . W1 + gy
   GemmRows gb{};

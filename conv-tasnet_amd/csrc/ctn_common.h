@@ -227,6 +227,82 @@ template <int NV> CTN_DEV void block_sum_d(double (&v)[NV], double* red) {
 }
 
 // ---------------------------------------------------------------------------
+// Statistics finalized by their consumer ("folded", gLN only): instead of a
+// separate finalize launch, every consumer workgroup reduces the producer's
+// partials of the utterances it needs (fold_stat: one canonical order, so all
+// workgroups agree bit for bit), and one designated workgroup stores the
+// finalized pairs for the kernels that follow.
+//
+// Partial layouts:
+//   dense   : slab[g * parts + i], i < parts
+//   WS runs : the persistent weight-stationary GEMM (ctn_gemm_ws.hip) gives
+//             workgroup b the tiles [t0(b), t0(b+1)), t0(b) = ntile*b/grid;
+//             each wave accumulates the consecutive tiles of one utterance and
+//             stores one partial per run: slab[((b*waves + w)*kmax + m - m0(b)],
+//             m0(b) = t0(b) / tpu (tpu = tiles per utterance)
+// ---------------------------------------------------------------------------
+struct WsRuns {
+  int ntile = 0, grid = 0, tpu = 1, waves = 0, kmax = 0;   // grid == 0: dense layout
+};
+__host__ __device__ inline int ws_t0(const WsRuns& w, int b) { return (int)((long)w.ntile * b / w.grid); }
+// the workgroup whose range holds tile t (the last b with t0(b) <= t)
+__host__ __device__ inline int ws_block_of_tile(const WsRuns& w, int t) {
+  return (int)(((long)(t + 1) * w.grid + w.ntile - 1) / w.ntile) - 1;
+}
+__host__ __device__ inline int ws_runs_kmax(int ntile, int grid, int tpu) {
+  const int twg = (ntile + grid - 1) / grid;
+  return (twg + tpu - 1) / tpu + 1;
+}
+
+struct StatFold {
+  const double2* slab = nullptr;   // producer partials; null: stats already final
+  int parts = 0;                   // dense layout: parts per group
+  double cnt = 1.0;                // elements per group
+  float eps = 0.f;
+  int mode = 0;                    // 0: (mean, rstd); 1: (S / cnt, SS / cnt)
+  float2* out = nullptr;           // finalized pairs [G] (may be null)
+  WsRuns ws;                       // WS run layout when ws.grid > 0
+};
+
+// Finalize group m, executed by a whole wave: lane l sums the group's partials
+// l, l+64, ... in order, then an xor butterfly (every lane ends with the same
+// bits, addition being commutative).
+CTN_DEV float2 fold_stat(const StatFold& f, int m) {
+  double s = 0.0, ss = 0.0;
+  const int lane = (int)(threadIdx.x & 63);
+  if (f.ws.grid == 0) {
+    const double2* sg = f.slab + (size_t)m * f.parts;
+    for (int i = lane; i < f.parts; i += 64) {
+      const double2 v = sg[i];
+      s += v.x;
+      ss += v.y;
+    }
+  } else {
+    const WsRuns& w = f.ws;
+    const int blo = ws_block_of_tile(w, m * w.tpu), bhi = ws_block_of_tile(w, (m + 1) * w.tpu - 1);
+    const int n = (bhi - blo + 1) * w.waves;
+    for (int i = lane; i < n; i += 64) {
+      const int b = blo + i / w.waves, wv = i % w.waves;
+      const int t0 = ws_t0(w, b);
+      if (t0 < ws_t0(w, b + 1)) {   // empty ranges stored nothing
+        const double2 v = f.slab[((size_t)b * w.waves + wv) * w.kmax + (m - t0 / w.tpu)];
+        s += v.x;
+        ss += v.y;
+      }
+    }
+  }
+  s = wave_sum(s);
+  ss = wave_sum(ss);
+  if (f.mode == 0) {
+    const double mean = s / f.cnt;
+    double var = ss / f.cnt - mean * mean;
+    if (var < 0.0) var = 0.0;
+    return make_float2((float)mean, (float)(1.0 / sqrt(var + (double)f.eps)));
+  }
+  return make_float2((float)(s / f.cnt), (float)(ss / f.cnt));
+}
+
+// ---------------------------------------------------------------------------
 // normalisation statistics: layout shared by all kernels
 //   gLN : one (mean, rstd) pair per utterance       index = m
 //   cLN : one (mean, rstd) pair per padded frame row index = row

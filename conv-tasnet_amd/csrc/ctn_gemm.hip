@@ -357,6 +357,19 @@ int gemm_rows_tiles_per_group(DType dt, const GemmRows& p) {
   return p.norm == NORM_GLN ? (p.g.Kp / rows_bm()) * ncol : ncol;
 }
 
+StatFold gemm_rows_stat_fold(DType dt, const GemmRows& p, const double2* slab, double cnt, float eps, int mode,
+                             float2* out) {
+  StatFold f;
+  f.slab = slab;
+  f.parts = gemm_rows_tiles_per_group(dt, p);
+  f.cnt = cnt;
+  f.eps = eps;
+  f.mode = mode;
+  f.out = out;
+  if (gemm_ws_eligible(dt, p) && p.norm == NORM_GLN) f.ws = gemm_ws_runs(p);
+  return f;
+}
+
 template <typename T, int OPK, int NK, int EPI>
 static hipError_t launch_rows_t(const GemmRows& p, hipStream_t s) {
   const int ncol = (p.Nout + RBN - 1) / RBN;

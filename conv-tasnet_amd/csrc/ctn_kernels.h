@@ -5,6 +5,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "ctn_common.h"
+
 namespace ctn {
 
 enum DType { F32 = 0, BF16 = 1 };
@@ -19,6 +21,7 @@ struct RowOp {
   const float* gamma = nullptr;
   const float* beta = nullptr;
   const float* alpha = nullptr;    // PReLU alpha (device pointer, 1 element)
+  StatFold fold;                   // gLN: finalize `stats` in the consumer (WS kernel only)
 };
 
 // Geometry of a frame-row tensor set: rows = M * Kp, valid frames K per utterance.
@@ -54,6 +57,11 @@ hipError_t launch_gemm_rows(DType dt, const GemmRows& p, hipStream_t s);
 bool gemm_ws_eligible(DType dt, const GemmRows& p);
 int gemm_ws_grid(const GemmRows& p);
 int gemm_ws_group_parts(const GemmRows& p);
+WsRuns gemm_ws_runs(const GemmRows& p);
+// StatFold for the group partials p's epilogue writes (WS run layout or dense)
+StatFold gemm_rows_stat_fold(DType dt, const GemmRows& p, const double2* slab, double cnt, float eps, int mode,
+                             float2* out);
+bool gemm_ws_can_fold(DType dt, const GemmRows& p);   // WS kernel and its operand stats fit the fold
 hipError_t launch_gemm_ws(const GemmRows& p, hipStream_t s);
 
 // ---- column GEMM (weight gradient): Cpart[chunk][p][q] = sum_r opA(A[r][p]) * opB(B[r][q])
@@ -126,6 +134,8 @@ struct DwArgs {
   const float2* sm1;                     // (ew) layer-1 sums
   void* gh1_out;                         // (ew) dL/dh1
   float* alpha_slab;                     // (ew) [blocks] galpha1 partials
+  // gLN folds (StatFold): dw_fwd finalizes st1, dw_bwd sm2, norm1_bwd sm1
+  StatFold f_st1, f_sm2, f_sm1;
 };
 int dw_seg(const DwArgs& a, bool bwd);   // comb segment length sizing one resident round
 int dw_blocks(const DwArgs& a);        // depthwise (comb) kernels (a.seg set)

@@ -127,7 +127,16 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
   const T* h1 = reinterpret_cast<const T*>(a.h1);
   T* dout = reinterpret_cast<T*>(a.d_out);
   const float al1 = a.alpha1[0], al2 = a.alpha2[0];
-  const float2 st1u = NK == NORM_GLN ? a.st1[it.m] : make_float2(0.f, 0.f);
+  float2 st1u = make_float2(0.f, 0.f);
+  if constexpr (NK == NORM_GLN) {
+    const StatFold& f = a.f_st1;
+    if (f.slab) {
+      st1u = fold_stat(f, it.m);
+      if (f.out && it.wgi == 0 && threadIdx.x == 0) f.out[it.m] = st1u;   // saved for backward
+    } else {
+      st1u = a.st1[it.m];
+    }
+  }
 
   float w[P][8], g1[8], b1[8];
 #pragma unroll
@@ -222,7 +231,12 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
   T* ga1o = reinterpret_cast<T*>(a.ga1_out);
   const float al1 = a.alpha1[0], al2 = a.alpha2[0];
   float2 st1u = make_float2(0.f, 0.f), st2u = st1u, sm2u = st1u;
-  if constexpr (NK == NORM_GLN) { st1u = a.st1[it.m]; st2u = a.st2[it.m]; sm2u = a.sm2[it.m]; }
+  if constexpr (NK == NORM_GLN) {
+    st1u = a.st1[it.m];
+    st2u = a.st2[it.m];
+    const StatFold& f = a.f_sm2;
+    sm2u = f.slab ? fold_stat(f, it.m) : a.sm2[it.m];
+  }
 
   float w[P][8], g1[8], b1[8], g2[8];
 #pragma unroll
@@ -399,6 +413,11 @@ __global__ __launch_bounds__(256) void norm1_bwd_kernel(DwArgs a) {
   T* gh = reinterpret_cast<T*>(a.gh1_out);
   const float al1 = a.alpha1[0];
   float calpha = 0.f;
+  float2 sm1u = make_float2(0.f, 0.f);
+  if constexpr (NK == NORM_GLN) {
+    const StatFold& f = a.f_sm1;
+    sm1u = f.slab ? fold_stat(f, m) : a.sm1[m];
+  }
   if (act) {
     for (int rr = rl; rr < DW_RPB; rr += nrl) {
       const int r = row0 + rr, k = r - base;
@@ -408,7 +427,7 @@ __global__ __launch_bounds__(256) void norm1_bwd_kernel(DwArgs a) {
         Vec8<T>::load(h1 + (size_t)r * H + c * 8, v);
         Vec8<T>::load(ga1 + (size_t)r * H + c * 8, g);
         const float2 st = ld_stat<NK>(a.st1, m, r);
-        const float2 sm = ld_stat<NK>(a.sm1, m, r);
+        const float2 sm = NK == NORM_GLN ? sm1u : a.sm1[r];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float ah = (prelu(v[e], al1) - st.x) * st.y;
