@@ -435,15 +435,25 @@ template <> CTN_DEV int cswz<bf16raw>(int row, int col) {
 }
 template <> CTN_DEV int cswz<float>(int row, int col) { return row * ColsPitch<float>::v + (col << 2); }
 
+// Two 4-wave groups per workgroup split a chunk's rows in halves, each with its
+// own LDS stages, and add their 128x128 accumulators through LDS at the end: one
+// partial per chunk from 8 waves halves the partial-sum traffic (write here, read
+// by the slab reduction) of 4-wave workgroups at the same occupancy.
+constexpr int CKS = 2;                           // k-split groups per workgroup
+constexpr int CTHREADS = 256 * CKS;
+
 template <typename T, int OPA, int OPB, int NK>
-__global__ __launch_bounds__(256) void gemm_cols_kernel(GemmCols p) {
+__global__ __launch_bounds__(CTHREADS) void gemm_cols_kernel(GemmCols p) {
   constexpr int PITCH = ColsPitch<T>::v;
   constexpr int STAGE = 2 * CKR * PITCH;         // one k-step: A tile then B tile
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  static_assert(CKS * 2 * STAGE >= (CKS - 1) * CBP * CBQ * 4, "accumulator exchange fits the stages");
+  __shared__ __attribute__((aligned(16))) char smem_all[CKS * 2 * STAGE];
   constexpr int E = Chunk<T>::E;
   constexpr int CPR = CBP * sizeof(T) / 16;      // 16-byte chunks per LDS row
   constexpr int NCH = CKR * CPR / 256;           // chunks per thread per operand
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int grp = threadIdx.x >> 8;              // k-split group
+  char* smem = smem_all + grp * 2 * STAGE;
+  const int tid = threadIdx.x & 255, lane = tid & 63, wid = tid >> 6;
   const int wp = wid >> 1, wq = wid & 1;
   const int lr = lane & 15, lg = lane >> 4;
 
@@ -454,10 +464,17 @@ __global__ __launch_bounds__(256) void gemm_cols_kernel(GemmCols p) {
 
   // 32-bit row arithmetic (M*Kp < 2^31; checked by the launcher): no 64-bit divisions
   const int rows = (int)p.g.rows();
-  const int rpc = (((rows + p.nchunks - 1) / p.nchunks + CKR - 1) / CKR) * CKR;   // rows per chunk, multiple of CKR
-  const int rbeg = chunk * rpc;
-  const int rend = rbeg + rpc < rows ? rbeg + rpc : rows;   // may be <= rbeg: empty chunk writes zeros
-  const int nks = rend > rbeg ? (rend - rbeg) / CKR : 0;    // k-steps (rows is a multiple of CKR)
+  const int rpc = (((rows + p.nchunks - 1) / p.nchunks + CKS * CKR - 1) / (CKS * CKR)) * (CKS * CKR);
+  const int half = rpc / CKS;                               // rows per group, multiple of CKR
+  const int cbeg = chunk * rpc;
+  const int steps_of = [&](int g) {
+    const int b = cbeg + g * half, e = b + half < rows ? b + half : rows;
+    return e > b ? (e - b) / CKR : 0;                       // rows is a multiple of CKR
+  }(0);
+  const int rbeg = cbeg + grp * half;
+  const int rend = rbeg + half < rows ? rbeg + half : rows;
+  const int nks = rend > rbeg ? (rend - rbeg) / CKR : 0;    // this group's k-steps (may be 0)
+  const int nks_all = steps_of;                             // group 0 holds the most steps
 
   const T* A = reinterpret_cast<const T*>(p.A);
   const T* B = reinterpret_cast<const T*>(p.B);
@@ -484,8 +501,9 @@ __global__ __launch_bounds__(256) void gemm_cols_kernel(GemmCols p) {
   // never straddles utterances (Kp % CKR == 0): one gLN statistic per step.
   constexpr int NST = NK == NORM_GLN ? 1 : NCH;
   struct Set { v4u a[NCH], b[NCH]; f32x2_t sa[NST], sb[NST]; };
+  const int last_r0 = nks > 0 ? rbeg + (nks - 1) * CKR : rows - CKR;   // clamp target (valid rows)
   auto gload = [&](Set& R, int ks) __attribute__((always_inline)) {
-    const int r0 = rbeg + (ks < nks ? ks : nks - 1) * CKR;
+    const int r0 = ks < nks ? rbeg + ks * CKR : last_r0;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int c = tid + 256 * i, rl = c / CPR;
@@ -618,34 +636,60 @@ __global__ __launch_bounds__(256) void gemm_cols_kernel(GemmCols p) {
   // Rows of padded frames are zero in the plain operands of this path, so they add
   // nothing; transformed operands are zeroed there explicitly.
   constexpr int NSET = 2;   // deeper rings measured slower (register pressure)
+  // Both groups run nks_all rounds in lock step (the barriers are workgroup-wide);
+  // a group with fewer steps keeps staging its clamped last step but skips the
+  // MFMAs of the surplus rounds (a wave-uniform branch after the barrier).
   auto run = [&](auto le1) __attribute__((always_inline)) {
     Set R[NSET];
 #pragma unroll
     for (int u = 0; u < NSET; ++u) gload(R[u], u);
     int ks = 0;
-    for (; ks + NSET - 1 < nks; ks += NSET) {   // full rounds: the same loads trail every wait
+    for (; ks + NSET - 1 < nks_all; ks += NSET) {   // full rounds: the same loads trail every wait
 #pragma unroll
       for (int u = 0; u < NSET; ++u) {
         swrite(le1, R[u], ks + u, smem + (u & 1) * STAGE);
         gload(R[u], ks + u + NSET);
         lds_barrier();
-        compute(smem + (u & 1) * STAGE);
+        if (ks + u < nks) compute(smem + (u & 1) * STAGE);
       }
     }
 #pragma unroll
     for (int u = 0; u < NSET; ++u) {   // tail (ks is a multiple of NSET, so parity = u & 1)
-      if (ks + u < nks) {
+      if (ks + u < nks_all) {
         swrite(le1, R[u], ks + u, smem + (u & 1) * STAGE);
         lds_barrier();
-        compute(smem + (u & 1) * STAGE);
+        if (ks + u < nks) compute(smem + (u & 1) * STAGE);
       }
     }
   };
-  if (nks > 0) {
+  if (nks_all > 0) {
     constexpr bool PR = OPA == OP_PRELU_NORM || OPB == OP_PRELU_NORM;
     if (!PR || (OPB == OP_PRELU_NORM ? alb : ala) <= 1.f) run(std::true_type{});
     else run(std::false_type{});
   }
+  // groups 1.. hand their accumulators to group 0 through LDS (the stages are free
+  // after this barrier), in group order: a fixed summation order
+  __syncthreads();
+  float* xch = reinterpret_cast<float*>(smem_all);
+  const int xi = (wid * 64 + lane) * 64;   // 64 accumulators per lane, lane-major
+  for (int g = 1; g < CKS; ++g) {
+    if (grp == g) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          *reinterpret_cast<f32x4_t*>(&xch[xi + (i * 4 + j) * 4]) = acc[i][j];
+    }
+    __syncthreads();
+    if (grp == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] += *reinterpret_cast<const f32x4_t*>(&xch[xi + (i * 4 + j) * 4]);
+    }
+    __syncthreads();
+  }
+  if (grp != 0) return;
   // lane holds D[p = p0 + wp*64 + i*16 + lg*4 + q][q = q0 + wq*64 + j*16 + lr]
   float* Cp = p.Cpart + (size_t)chunk * p.P * p.Q;
 #pragma unroll
@@ -665,8 +709,8 @@ __global__ __launch_bounds__(256) void gemm_cols_kernel(GemmCols p) {
 int gemm_cols_default_chunks(const GemmCols& p) {
   const int tiles = ((p.P + CBP - 1) / CBP) * ((p.Q + CBQ - 1) / CBQ);
   const long rows = p.g.rows();
-  int ch = (512 + tiles - 1) / tiles;            // ~512 workgroups
-  const long maxch = (rows + CKR * 4 - 1) / (CKR * 4);   // >= 4 k-steps per chunk
+  int ch = (256 + tiles - 1) / tiles;            // ~256 workgroups of CKS x 4 waves
+  const long maxch = (rows + CKS * CKR * 4 - 1) / (CKS * CKR * 4);   // >= 4 k-steps per group
   if (ch > maxch) ch = (int)maxch;
   return ch < 1 ? 1 : ch;
 }
@@ -674,7 +718,7 @@ int gemm_cols_default_chunks(const GemmCols& p) {
 template <typename T, int OPA, int OPB, int NK>
 static hipError_t launch_cols_t(const GemmCols& p, hipStream_t s) {
   const int tiles = ((p.P + CBP - 1) / CBP) * ((p.Q + CBQ - 1) / CBQ);
-  hipLaunchKernelGGL((gemm_cols_kernel<T, OPA, OPB, NK>), dim3(tiles * p.nchunks), dim3(256), 0, s, p);
+  hipLaunchKernelGGL((gemm_cols_kernel<T, OPA, OPB, NK>), dim3(tiles * p.nchunks), dim3(CTHREADS), 0, s, p);
   return hipGetLastError();
 }
 
