@@ -82,8 +82,14 @@ class ConvTasNet(nn.Module):
         cln, bott = sep.network[0], sep.network[1]
         w_rows, x = ops.EncoderFn.apply(mixture, fr, (self.N, self.L, self.B, self.C), dt,
                                         self.encoder.conv1d_U.weight, cln.gamma, cln.beta, bott.weight)
-        for blk in sep.blocks():
-            x = blk._forward_rows(x, fr, norm)
+        blocks = list(sep.blocks())
+        packs = [None] * len(blocks)
+        if dt == torch.bfloat16:   # bf16 weight copies for every block: one launch per step
+            if not hasattr(self, "_packs"):
+                self._packs = ops.WeightPacks()
+            packs = self._packs.get([(b.net[0].weight, b._params()[8]) for b in blocks], mixture.device)
+        for blk, pk in zip(blocks, packs):
+            x = blk._forward_rows(x, fr, norm, pk)
         return ops.DecoderFn.apply(x, w_rows, fr, (T, self.N, self.L, self.B, self.C, _mask_code(self.mask_nonlinear)),
                                    sep.network[3].weight, self.decoder.basis_signals.weight)
 
@@ -223,9 +229,9 @@ class TemporalBlock(nn.Module):
         return (self.net[0].weight, self.net[1].weight, n1.gamma, n1.beta, ds[0].weight,
                 ds[1 + off].weight, n2.gamma, n2.beta, ds[3 + off].weight)
 
-    def _forward_rows(self, x_rows, fr, norm):
+    def _forward_rows(self, x_rows, fr, norm, pack=None):
         B, H, P, dil, causal, _ = self._geo
-        return ops.TBlockFn.apply(x_rows, fr, (B, H, P, dil, causal, norm), *self._params())
+        return ops.TBlockFn.apply(x_rows, fr, (B, H, P, dil, causal, norm), pack, *self._params())
 
     def forward(self, x):
         """x [M, B, K] -> [M, B, K]."""

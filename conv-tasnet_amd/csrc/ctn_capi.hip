@@ -256,7 +256,10 @@ extern "C" int ctn_tblock_forward(const ctn_tblock_desc* d, const ctn_tblock_par
 
   const void* w1 = p->w1;
   const void* w2 = p->w2;
-  if (dt == BF16) {
+  if (dt == BF16 && p->w1_bf16 && p->w2_bf16) {   // packed once per step by the caller
+    w1 = p->w1_bf16;
+    w2 = p->w2_bf16;
+  } else if (dt == BF16) {
     PrepBatch pb{};
     pb.d[0] = PrepDesc{p->w1, d->H, d->B, L.w1s, nullptr};
     pb.d[1] = PrepDesc{p->w2, d->B, d->H, L.w2s, nullptr};
@@ -322,7 +325,12 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
   const float2* st2 = st1 + G;
   const double cnt = d->norm_type == CTN_NORM_GLN ? (double)d->K * d->H : (double)d->H;
 
-  {
+  const void* w1t = L.w1t;
+  const void* w2t = L.w2t;
+  if (dt == BF16 && p->w1t_bf16 && p->w2t_bf16) {   // packed once per step by the caller
+    w1t = p->w1t_bf16;
+    w2t = p->w2t_bf16;
+  } else {
     PrepBatch pb{};
     pb.d[0] = PrepDesc{p->w2, d->B, d->H, nullptr, L.w2t};   // [H][B]
     pb.d[1] = PrepDesc{p->w1, d->H, d->B, nullptr, L.w1t};   // [B][H]
@@ -333,7 +341,7 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
   // (a) G1 = g_n2 = gy . W2 ; epilogue: norm-2 backward sums of (g_n2*gamma2, g_n2*gamma2*hat a2)
   GemmRows ga = tb_gemmA(d);
   ga.A = gy;
-  ga.W = L.w2t;
+  ga.W = w2t;
   ga.R = sv->d;
   ga.alpha = p->alpha2; ga.stats = st2; ga.gamma = p->gamma2;
   ga.C = L.G1;
@@ -375,7 +383,7 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
   GemmRows gb{};
   gb.g = rg; gb.Kred = d->H; gb.Nout = d->B; gb.norm = d->norm_type;
   gb.A = L.G1; gb.lda = d->H;
-  gb.W = L.w1t; gb.ldw = d->H;
+  gb.W = w1t; gb.ldw = d->H;
   gb.epi = EPI_RESID; gb.R = gy; gb.ldr = d->B;
   gb.C = gx; gb.ldc = d->B;
   CTN_HIP(launch_gemm_rows(dt, gb, s));
@@ -782,5 +790,27 @@ extern "C" int ctn_adam_step(const ctn_opt_segment* segs, const ctn_opt_chunk* c
   AdamArgs a{hp->beta1, hp->beta2, hp->eps, hp->weight_decay, (float)(hp->lr / bc1), (float)sqrt(bc2)};
   CTN_HIP(launch_adam(reinterpret_cast<const OptSegment*>(segs), reinterpret_cast<const OptChunk*>(chunks), nchunks,
                       a, (hipStream_t)stream));
+  return CTN_OK;
+}
+
+// ===========================================================================
+// Weight packing (bf16 compute copies for a whole step)
+// ===========================================================================
+static_assert(sizeof(ctn_weight_pack) == sizeof(PrepDesc), "pack layout");
+
+extern "C" int ctn_pack_weights(const ctn_weight_pack* packs, int n, void* stream) {
+  if (n < 0 || (n > 0 && !packs)) return fail(CTN_ERR_ARG, "ctn_pack_weights: bad table");
+  for (int i = 0; i < n; ++i)
+    if (!packs[i].src || packs[i].rows <= 0 || packs[i].cols <= 0 || (!packs[i].dst && !packs[i].dst_t))
+      return fail(CTN_ERR_ARG, "ctn_pack_weights: entry %d is empty or has no destination", i);
+  for (int i0 = 0; i0 < n; i0 += PREP_MAX) {
+    PrepBatch pb{};
+    pb.nd = n - i0 < PREP_MAX ? n - i0 : PREP_MAX;
+    for (int i = 0; i < pb.nd; ++i) {
+      const ctn_weight_pack& w = packs[i0 + i];
+      pb.d[i] = PrepDesc{w.src, w.rows, w.cols, w.dst, w.dst_t};
+    }
+    CTN_HIP(launch_prep_weights(BF16, pb, (hipStream_t)stream));
+  }
   return CTN_OK;
 }

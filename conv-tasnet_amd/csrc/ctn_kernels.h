@@ -104,8 +104,9 @@ struct PrepDesc {
   void* Ws;
   void* Wt;
 };
+constexpr int PREP_MAX = 64;   // descriptors per launch (kernel-argument budget)
 struct PrepBatch {
-  PrepDesc d[4];
+  PrepDesc d[PREP_MAX];
   int nd;
 };
 hipError_t launch_prep_weights(DType dt, const PrepBatch& pb, hipStream_t s);   // one launch

@@ -654,28 +654,46 @@ hipError_t launch_slab_reduce(const SlabBatch& b, float* tmp, hipStream_t s) {
   return sr_launch(p2, s);
 }
 
+// fp32 [O][I] weight -> storage-type copy Ws [O][I] and/or transpose Wt [I][O], one
+// 64x64 tile per workgroup through LDS: both the row-major reads/writes and the
+// transposed writes are coalesced.  grid = (tiles of the largest matrix, nd).
+constexpr int PW_T = 64;
 template <typename T>
 __global__ __launch_bounds__(256) void prep_weight_kernel(PrepBatch pb) {
+  __shared__ float tile[PW_T][PW_T + 1];
   const PrepDesc d = pb.d[blockIdx.y];
-  const long n = (long)d.O * d.I;
+  const int tcol = (d.I + PW_T - 1) / PW_T, trow = (d.O + PW_T - 1) / PW_T;
+  if ((int)blockIdx.x >= tcol * trow) return;
+  const int r0 = (blockIdx.x / tcol) * PW_T, c0 = (blockIdx.x % tcol) * PW_T;
   T* Ws = reinterpret_cast<T*>(d.Ws);
   T* Wt = reinterpret_cast<T*>(d.Wt);
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
-    const int o = (int)(i / d.I), j = (int)(i % d.I);
-    const float v = d.W[i];
-    if (Ws) st1<T>(Ws + i, v);
-    if (Wt) st1<T>(Wt + (size_t)j * d.O + o, v);
+  for (int i = threadIdx.x; i < PW_T * PW_T; i += 256) {
+    const int r = i / PW_T, c = i % PW_T;
+    float v = 0.f;
+    if (r0 + r < d.O && c0 + c < d.I) {
+      v = d.W[(size_t)(r0 + r) * d.I + c0 + c];
+      if (Ws) st1<T>(Ws + (size_t)(r0 + r) * d.I + c0 + c, v);
+    }
+    tile[r][c] = v;
+  }
+  if (!Wt) return;
+  __syncthreads();
+  for (int i = threadIdx.x; i < PW_T * PW_T; i += 256) {
+    const int c = i / PW_T, r = i % PW_T;
+    if (r0 + r < d.O && c0 + c < d.I) st1<T>(Wt + (size_t)(c0 + c) * d.O + r0 + r, tile[r][c]);
   }
 }
 
 hipError_t launch_prep_weights(DType dt, const PrepBatch& pb, hipStream_t s) {
   if (pb.nd <= 0) return hipSuccess;
-  long mx = 1;
-  for (int i = 0; i < pb.nd; ++i) mx = (long)pb.d[i].O * pb.d[i].I > mx ? (long)pb.d[i].O * pb.d[i].I : mx;
-  int g = (int)((mx + 255) / 256);
-  if (g > 512) g = 512;
-  if (dt == BF16) hipLaunchKernelGGL(prep_weight_kernel<bf16raw>, dim3(g, pb.nd), dim3(256), 0, s, pb);
-  else hipLaunchKernelGGL(prep_weight_kernel<float>, dim3(g, pb.nd), dim3(256), 0, s, pb);
+  if (pb.nd > PREP_MAX) return hipErrorInvalidValue;
+  int mx = 1;
+  for (int i = 0; i < pb.nd; ++i) {
+    const int t = ((pb.d[i].O + PW_T - 1) / PW_T) * ((pb.d[i].I + PW_T - 1) / PW_T);
+    mx = t > mx ? t : mx;
+  }
+  if (dt == BF16) hipLaunchKernelGGL(prep_weight_kernel<bf16raw>, dim3(mx, pb.nd), dim3(256), 0, s, pb);
+  else hipLaunchKernelGGL(prep_weight_kernel<float>, dim3(mx, pb.nd), dim3(256), 0, s, pb);
   return hipGetLastError();
 }
 

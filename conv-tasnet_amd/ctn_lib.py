@@ -14,7 +14,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CTN_HIP_LIB", os.path.join(_HERE, "libctn_hip.so"))
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 DTYPE_F32, DTYPE_BF16 = 0, 1
 NORM_GLN, NORM_CLN = 0, 1
@@ -40,7 +40,11 @@ _TB_PARAM_NAMES = ("w1", "alpha1", "gamma1", "beta1", "wd", "alpha2", "gamma2", 
 
 
 class TBlockParams(ctypes.Structure):
-    _fields_ = [(n, c_void_p) for n in _TB_PARAM_NAMES]
+    _fields_ = [(n, c_void_p) for n in _TB_PARAM_NAMES + ("w1_bf16", "w2_bf16", "w1t_bf16", "w2t_bf16")]
+
+
+class WeightPack(ctypes.Structure):
+    _fields_ = [("src", c_void_p), ("rows", c_int32), ("cols", c_int32), ("dst", c_void_p), ("dst_t", c_void_p)]
 
 
 class TBlockGrads(ctypes.Structure):
@@ -99,6 +103,7 @@ _SIGS = {
     "ctn_pit_workspace_bytes": (c_size_t, [c_void_p]),
     "ctn_pit_forward": (ctypes.c_int, [c_void_p] + [c_void_p] * 8 + [c_void_p, c_size_t, c_void_p]),
     "ctn_pit_backward": (ctypes.c_int, [c_void_p] + [c_void_p] * 7 + [c_void_p]),
+    "ctn_pack_weights": (ctypes.c_int, [c_void_p, ctypes.c_int, c_void_p]),
     "ctn_opt_plan": (ctypes.c_int, [c_void_p, ctypes.c_int, c_void_p, ctypes.c_int]),
     "ctn_grad_clip_norm": (ctypes.c_int, [c_void_p, c_void_p, ctypes.c_int, ctypes.c_float, c_void_p, c_void_p,
                                           c_void_p]),

@@ -36,16 +36,62 @@ def _f32(t: torch.Tensor) -> torch.Tensor:
 # ----------------------------------------------------------------------------
 # TemporalBlock (conv_tasnet.py:212-272)
 # ----------------------------------------------------------------------------
+class WeightPacks:
+    """bf16 compute copies of the TemporalBlocks' 1x1 weights (W1 [H,B], W2 [B,H]
+    and both transposes), refreshed for all stale blocks in ONE native call per
+    step (ctn_pack_weights) instead of a conversion inside every block call.
+    A copy is stale when its fp32 parameter's version counter moved: every
+    in-place update bumps it (torch optimizers, load_state_dict, and
+    ctn_optim.Adam, which bumps it explicitly)."""
+
+    def __init__(self):
+        self.key = None
+        self.buf = None
+        self.vers = []
+        self.ptrs = []
+
+    def get(self, pairs: list, device) -> list:
+        """pairs: [(w1, w2)] fp32 parameters -> [(w1s, w2s, w1t, w2t) device pointers]."""
+        key = (device, tuple((w1.data_ptr(), w2.data_ptr(), tuple(w1.shape), tuple(w2.shape)) for w1, w2 in pairs))
+        if key != self.key:
+            sizes = [(w1.numel(), w2.numel()) for w1, w2 in pairs]
+            total = sum(2 * (a + b) for a, b in sizes)
+            self.buf = torch.empty(total, dtype=torch.bfloat16, device=device)
+            base, off, self.ptrs = self.buf.data_ptr(), 0, []
+            for a, b in sizes:
+                w1s, w2s, w1t, w2t = (base + 2 * o for o in (off, off + a, off + a + b, off + 2 * a + b))
+                self.ptrs.append((w1s, w2s, w1t, w2t))
+                off += 2 * (a + b)
+            self.key = key
+            self.vers = [None] * len(pairs)
+        packs = []
+        for i, (w1, w2) in enumerate(pairs):
+            v = (w1._version, w2._version)
+            if self.vers[i] != v:
+                w1s, w2s, w1t, w2t = self.ptrs[i]
+                H, B = w1.shape[0], w1.shape[1]
+                packs.append(L.WeightPack(_f32(w1).data_ptr(), H, B, w1s, w1t))
+                packs.append(L.WeightPack(_f32(w2).data_ptr(), B, H, w2s, w2t))
+                self.vers[i] = v
+        if packs:
+            arr = (L.WeightPack * len(packs))(*packs)
+            L.check(L.load().ctn_pack_weights(arr, len(packs), L.stream_handle(device)), "ctn_pack_weights")
+        return self.ptrs
+
+
 class TBlockFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, fr: Frames, cfg: tuple, w1, a1, g1, b1, wd, a2, g2, b2, w2):
+    def forward(ctx, x, fr: Frames, cfg: tuple, pack, w1, a1, g1, b1, wd, a2, g2, b2, w2):
+        """pack: (w1s, w2s, w1t, w2t) bf16 copies from WeightPacks, or None."""
         B, H, P, dil, causal, norm = cfg
         lib = L.load()
         L.require_device(x, "TemporalBlock")
         x = x.contiguous()
         params = [_f32(t) for t in (w1, a1, g1, b1, wd, a2, g2, b2, w2)]
         desc = L.TBlockDesc(fr.M, fr.K, fr.Kp, B, H, P, dil, int(causal), norm, L.dtype_code(x.dtype))
-        pstruct = L.TBlockParams(*[p.data_ptr() for p in params])
+        pack = pack if x.dtype == torch.bfloat16 else None
+        ctx.pack = pack
+        pstruct = L.TBlockParams(*[p.data_ptr() for p in params], *(pack or (None,) * 4))
         y = torch.empty_like(x)
         h1 = x.new_empty(fr.rows, H)
         d = x.new_empty(fr.rows, H)
@@ -69,7 +115,7 @@ class TBlockFn(torch.autograd.Function):
         if gy.dtype != x.dtype:
             gy = gy.to(x.dtype)
         desc = L.TBlockDesc(*ctx.desc)
-        pstruct = L.TBlockParams(*[p.data_ptr() for p in params])
+        pstruct = L.TBlockParams(*[p.data_ptr() for p in params], *(ctx.pack or (None,) * 4))
         saved = L.TBlockSaved(h1.data_ptr(), d.data_ptr(), stats.data_ptr())
         gx = torch.empty_like(x)
         grads = [torch.empty_like(p) for p in params]
@@ -80,7 +126,7 @@ class TBlockFn(torch.autograd.Function):
                                         ctypes.byref(saved), gy.data_ptr(), gx.data_ptr(), ctypes.byref(gstruct),
                                         ws.data_ptr(), nb, L.stream_handle(x.device)),
                 "ctn_tblock_backward")
-        return (gx, None, None, *grads)
+        return (gx, None, None, None, *grads)
 
 
 # ----------------------------------------------------------------------------

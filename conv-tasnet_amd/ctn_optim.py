@@ -83,6 +83,7 @@ def _check_tensor(t: torch.Tensor, what: str):
 
 
 _clip_plans: OrderedDict = OrderedDict()
+_bump = torch.autograd.graph.increment_version
 
 
 @torch.no_grad()
@@ -111,6 +112,8 @@ def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0, error_i
     L.check(L.load().ctn_grad_clip_norm(segs_dev.data_ptr(), plan.chunks.data_ptr(), plan.nchunks,
                                         float(max_norm), total.data_ptr(), plan.partial.data_ptr(),
                                         L.stream_handle(dev)), "ctn_grad_clip_norm")
+    for g in grads:
+        _bump(g)
     if error_if_nonfinite and not bool(torch.isfinite(total)):
         raise RuntimeError(f"The total norm of order {float(norm_type)} for gradients from `parameters` "
                            f"is non-finite, so it cannot be clipped.")
@@ -195,4 +198,9 @@ class Adam(torch.optim.Optimizer):
                                    float(group["weight_decay"]), n)
                 L.check(lib.ctn_adam_step(segs_dev.data_ptr(), plan.chunks.data_ptr(), plan.nchunks,
                                           ctypes.byref(hp), L.stream_handle(dev)), "ctn_adam_step")
+                # the kernel wrote through raw pointers: bump the parameters' version
+                # counters as an in-place torch update would (autograd's saved-tensor
+                # checks; derived weight copies such as ctn_ops.WeightPacks)
+                for p, _, _, _ in items:
+                    _bump(p)
         return loss

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define CTN_ABI_VERSION 1
+#define CTN_ABI_VERSION 2
 
 typedef enum { CTN_DTYPE_F32 = 0, CTN_DTYPE_BF16 = 1 } ctn_dtype;
 typedef enum { CTN_NORM_GLN = 0, CTN_NORM_CLN = 1 } ctn_norm_type;
@@ -75,7 +75,25 @@ typedef struct {            /* fp32 device pointers, reference shapes */
   const float* gamma2;      /* [1,H,1] net.3.net.{2|3}.gamma */
   const float* beta2;       /* [1,H,1] net.3.net.{2|3}.beta */
   const float* w2;          /* [B,H,1] net.3.net.{3|4}.weight */
+  /* optional bf16 compute copies made by ctn_pack_weights (dtype BF16 only; NULL:
+   * the call converts w1/w2 itself): W1 [H][B], W2 [B][H] and their transposes */
+  const void* w1_bf16;
+  const void* w2_bf16;
+  const void* w1t_bf16;     /* [B][H] */
+  const void* w2t_bf16;     /* [H][B] */
 } ctn_tblock_params;
+
+/* One fp32 weight [rows][cols] -> bf16 copy (dst, same layout) and/or bf16
+ * transpose (dst_t, [cols][rows]); either may be NULL. */
+typedef struct {
+  const float* src;
+  int32_t rows, cols;
+  void* dst;
+  void* dst_t;
+} ctn_weight_pack;
+/* Converts n weights in ceil(n / 64) launches (a training step's bf16 weight
+ * copies for all TemporalBlocks at once, instead of per block call). */
+int ctn_pack_weights(const ctn_weight_pack* packs, int n, void* stream);
 
 typedef struct {            /* fp32 outputs, same shapes as ctn_tblock_params */
   float *w1, *alpha1, *gamma1, *beta1, *wd, *alpha2, *gamma2, *beta2, *w2;

@@ -30,7 +30,7 @@ def run_block(x_ncw, params, P, dil, causal, norm, G_ncw, dtype=torch.float32):
     x = ops.ncw_to_rows(x_ncw.to(DEV), fr, dtype).requires_grad_(True)
     ps = [p.to(DEV).float().clone().requires_grad_(True) for p in params]
     cfg = (B, H, P, dil, causal, L.NORM_GLN if norm == "gLN" else L.NORM_CLN)
-    y = ops.TBlockFn.apply(x, fr, cfg, *ps)
+    y = ops.TBlockFn.apply(x, fr, cfg, None, *ps)
     y_ncw = ops.rows_to_ncw(y, fr, torch.float32)
     (y_ncw * G_ncw.to(DEV)).sum().backward()
     gx = ops.rows_to_ncw(x.grad, fr, torch.float32)
@@ -106,3 +106,36 @@ def test_tblock_paper_dims_vs_oracle(dtype, tol, d, causal, norm):
             # O(1) relative noise in it.  Its fp32 parity is checked above (dtype=f32).
             continue
         assert rel(gg.reshape(pd[n].shape), pd[n].grad) < tol * 5, n
+
+
+def test_weight_packs_match_per_call_conversion():
+    """bf16 weight copies packed once per step (ctn_pack_weights) give bit-identical
+    results to the per-call conversion, and refresh when the fp32 weight changes."""
+    import ctn_lib as L
+    import ctn_ops as ops
+    torch.manual_seed(0)
+    params = _paper_block(3)
+    M, B, K = 2, 256, 700
+    fr = ops.Frames.of(M, K)
+    x = ops.ncw_to_rows(torch.randn(M, B, K, device=DEV), fr, torch.bfloat16)
+    cfg = (B, 512, 3, 4, False, L.NORM_GLN)
+    ps = [p.to(DEV).clone().requires_grad_(True) for p in params]
+    packs = ops.WeightPacks()
+
+    def run(pack):
+        for p in ps:
+            p.grad = None
+        xx = x.clone().requires_grad_(True)
+        y = ops.TBlockFn.apply(xx, fr, cfg, pack, *ps)
+        y.float().square().sum().backward()
+        return y.detach(), xx.grad.detach(), [p.grad.detach().clone() for p in ps]
+
+    for step in range(2):
+        ref = run(None)
+        got = run(packs.get([(ps[0], ps[8])], x.device)[0])
+        assert torch.equal(ref[0], got[0]) and torch.equal(ref[1], got[1])
+        for a, b in zip(ref[2], got[2]):
+            assert torch.equal(a, b)
+        with torch.no_grad():   # in-place update: the packed copy must refresh
+            ps[0].mul_(0.5)
+            ps[8].add_(0.01)
