@@ -16,9 +16,9 @@ import sys
 from collections import defaultdict
 
 KINDS = {   # bench.py timer kinds -> kernel name (bf16 throughput mode)
-    "1": "ctn::gemm_rows_kernel<unsigned short, 0, 0, 1, 64>",
+    "1": "ctn::gemm_ws_kernel<0, 0, 1, 2, 8, 16, 2>",
     "2": "ctn::dw_fwd_kernel<unsigned short, 0, 3, false>",
-    "3": "ctn::gemm_rows_kernel<unsigned short, 0, 0, 3, 64>",
+    "3": "ctn::gemm_ws_kernel<0, 0, 3, 4, 8, 8, 1>",
 }
 
 
