@@ -1,3 +1,4 @@
+#include <stdlib.h>
 // extern "C" entry points of libctn_hip.so (include/ctn.h) and the native
 // launch sequences behind them.  Each entry validates its descriptor, carves
 // the caller's workspace, and enqueues its kernels on the caller's stream.
@@ -179,6 +180,28 @@ GemmRows tb_gemmA(const ctn_tblock_desc* d) {   // backward g_n2 = gy . W2, norm
   return g;
 }
 
+// The backward's two dual GEMMs (ctn_gemm_dual.hip), shapes and operand ops only:
+//   A: g_n2 = gy . W2 (norm-2 backward epilogue) + dW2 = gy^T . norm2(PReLU(d))
+//   B: gx = gh1 . W1 + gy                        + dW1 = gh1^T . x
+GemmDual tb_dualA(const ctn_tblock_desc* d) {
+  GemmDual g{};
+  g.g = Rows{d->M, d->K, d->Kp};
+  g.Kred = d->B; g.Nout = d->H; g.norm = d->norm_type;
+  g.lda = d->B; g.ldw = d->B; g.ldc = d->H; g.ldr = d->H; g.ldb = d->H;
+  g.epi = EPI_NORM_BWD;
+  g.bop.kind = OP_PRELU_NORM; g.bop.norm = d->norm_type;
+  return g;
+}
+GemmDual tb_dualB(const ctn_tblock_desc* d) {
+  GemmDual g{};
+  g.g = Rows{d->M, d->K, d->Kp};
+  g.Kred = d->H; g.Nout = d->B; g.norm = d->norm_type;
+  g.lda = d->H; g.ldw = d->H; g.ldc = d->B; g.ldr = d->B; g.ldb = d->B;
+  g.epi = EPI_RESID;
+  return g;
+}
+DType tb_dt(const ctn_tblock_desc* d) { return d->dtype == CTN_DTYPE_BF16 ? BF16 : F32; }
+
 TbLayout tb_layout(const ctn_tblock_desc* d, int backward, void* ws) {
   TbLayout L{};
   Carver c(ws);
@@ -207,7 +230,9 @@ TbLayout tb_layout(const ctn_tblock_desc* d, int backward, void* ws) {
     L.G1 = c.take<void>((size_t)rows * d->H * es);
     L.G2 = c.take<void>((size_t)rows * d->H * es);
     GemmRows ga = tb_gemmA(d);
-    L.partsA = gemm_rows_tiles_per_group(dtl, ga);
+    const GemmDual duA = tb_dualA(d), duB = tb_dualB(d);
+    const bool dualA = gemm_dual_eligible(dtl, duA), dualB = gemm_dual_eligible(dtl, duB);
+    L.partsA = dualA ? gemm_dual_group_parts(duA) : gemm_rows_tiles_per_group(dtl, ga);
     L.slabA = c.take<double2>((size_t)G * L.partsA * sizeof(double2));
     L.partsD = dw_parts_per_group(da);
     L.slabD = c.take<double2>((size_t)G * L.partsD * sizeof(double2));
@@ -217,10 +242,10 @@ TbLayout tb_layout(const ctn_tblock_desc* d, int backward, void* ws) {
     L.sums2 = c.take<float2>((size_t)G * sizeof(float2));
     GemmCols gc{};
     gc.g = rg; gc.P = d->B; gc.Q = d->H;
-    L.chunks2 = gemm_cols_default_chunks(gc);
+    L.chunks2 = dualA ? gemm_dual_ranges(duA) : gemm_cols_default_chunks(gc);
     L.cpart2 = c.take<float>((size_t)L.chunks2 * d->B * d->H * sizeof(float));
     gc.P = d->H; gc.Q = d->B;
-    L.chunks1 = gemm_cols_default_chunks(gc);
+    L.chunks1 = dualB ? gemm_dual_ranges(duB) : gemm_cols_default_chunks(gc);
     L.cpart1 = c.take<float>((size_t)L.chunks1 * d->B * d->H * sizeof(float));
     const long HB = (long)d->H * d->B, dwb = dw_blocks(da);
     const size_t ntmp = sr_tmp(L.chunks2, HB) + sr_tmp(L.chunks1, HB) + 4 * sr_tmp(dwb, d->H) +
@@ -339,6 +364,7 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
   }
 
   // (a) G1 = g_n2 = gy . W2 ; epilogue: norm-2 backward sums of (g_n2*gamma2, g_n2*gamma2*hat a2)
+  // (b) dW2 = gy^T . norm2(PReLU(d))            — one dual-GEMM pass when eligible
   GemmRows ga = tb_gemmA(d);
   ga.A = gy;
   ga.W = w2t;
@@ -346,21 +372,32 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
   ga.alpha = p->alpha2; ga.stats = st2; ga.gamma = p->gamma2;
   ga.C = L.G1;
   ga.grp_slab = L.slabA;
-  {
+  GemmDual duA = tb_dualA(d);
+  duA.A = gy; duA.W = w2t; duA.R = sv->d; duA.C = L.G1;
+  duA.alpha = p->alpha2; duA.stats = st2; duA.gamma = p->gamma2; duA.grp_slab = L.slabA;
+  duA.Bm = sv->d;
+  duA.bop.stats = st2; duA.bop.gamma = p->gamma2; duA.bop.beta = p->beta2; duA.bop.alpha = p->alpha2;
+  duA.Dpart = L.cpart2;
+  const bool dualA = gemm_dual_eligible(dt, duA);
+  if (dualA) {
     TimedScope ts(3, s);
-    CTN_HIP(launch_gemm_rows(dt, ga, s));
+    CTN_HIP(launch_gemm_dual(duA, s));
+  } else {
+    {
+      TimedScope ts(3, s);
+      CTN_HIP(launch_gemm_rows(dt, ga, s));
+    }
+    GemmCols c2{};
+    c2.g = rg; c2.P = d->B; c2.Q = d->H;
+    c2.A = gy; c2.lda = d->B;
+    c2.B = sv->d; c2.ldb = d->H;
+    c2.bop.kind = OP_PRELU_NORM; c2.bop.norm = d->norm_type; c2.bop.stats = st2;
+    c2.bop.gamma = p->gamma2; c2.bop.beta = p->beta2; c2.bop.alpha = p->alpha2;
+    c2.Cpart = L.cpart2; c2.nchunks = L.chunks2;
+    CTN_HIP(launch_gemm_cols(dt, c2, s));
   }
   const bool fold = d->norm_type == CTN_NORM_GLN;   // gLN: consumers finalize the sums (StatFold)
   if (!fold) CTN_HIP(launch_stats_finalize(L.slabA, G, L.partsA, cnt, 1, 0.f, L.sums2, s));
-  // (b) dW2 = gy^T . norm2(PReLU(d))
-  GemmCols c2{};
-  c2.g = rg; c2.P = d->B; c2.Q = d->H;
-  c2.A = gy; c2.lda = d->B;
-  c2.B = sv->d; c2.ldb = d->H;
-  c2.bop.kind = OP_PRELU_NORM; c2.bop.norm = d->norm_type; c2.bop.stats = st2;
-  c2.bop.gamma = p->gamma2; c2.bop.beta = p->beta2; c2.bop.alpha = p->alpha2;
-  c2.Cpart = L.cpart2; c2.nchunks = L.chunks2;
-  CTN_HIP(launch_gemm_cols(dt, c2, s));
   // (c) depthwise backward -> G2 = dL/d(hat a1), norm1 sums, column partials (gamma1/beta1,
   //     wd, gamma2/beta2, alpha2)
   DwArgs da{};
@@ -370,7 +407,9 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
   da.alpha1 = p->alpha1; da.gamma1 = p->gamma1; da.beta1 = p->beta1; da.alpha2 = p->alpha2; da.gamma2 = p->gamma2;
   da.wd = p->wd;
   da.ga2 = L.G1; da.sm2 = L.sums2; da.ga1_out = L.G2; da.slab1 = L.slabD; da.col_slab = L.colD;
-  if (fold) da.f_sm2 = gemm_rows_stat_fold(dt, ga, L.slabA, cnt, 0.f, 1, nullptr);
+  if (fold)
+    da.f_sm2 = dualA ? gemm_dual_stat_fold(duA, L.slabA, cnt, 0.f, 1, nullptr)
+                     : gemm_rows_stat_fold(dt, ga, L.slabA, cnt, 0.f, 1, nullptr);
   CTN_HIP(launch_dw_bwd(dt, da, s));
   if (!fold) CTN_HIP(launch_stats_finalize(L.slabD, G, L.partsD, cnt, 1, 0.f, L.sums1, s));
   // (d) norm1 backward finish + PReLU1 backward -> G1 = dL/dh1
@@ -380,20 +419,27 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
   if (fold) de.f_sm1 = StatFold{L.slabD, L.partsD, cnt, 0.f, 1, nullptr};
   CTN_HIP(launch_norm1_bwd(dt, de, s));
   // (e) gx = gh1 . W1 + gy
-  GemmRows gb{};
-  gb.g = rg; gb.Kred = d->H; gb.Nout = d->B; gb.norm = d->norm_type;
-  gb.A = L.G1; gb.lda = d->H;
-  gb.W = w1t; gb.ldw = d->H;
-  gb.epi = EPI_RESID; gb.R = gy; gb.ldr = d->B;
-  gb.C = gx; gb.ldc = d->B;
-  CTN_HIP(launch_gemm_rows(dt, gb, s));
-  // (f) dW1 = gh1^T . x
-  GemmCols c1{};
-  c1.g = rg; c1.P = d->H; c1.Q = d->B;
-  c1.A = L.G1; c1.lda = d->H;
-  c1.B = x; c1.ldb = d->B;
-  c1.Cpart = L.cpart1; c1.nchunks = L.chunks1;
-  CTN_HIP(launch_gemm_cols(dt, c1, s));
+  // (f) dW1 = gh1^T . x                          — one dual-GEMM pass when eligible
+  GemmDual duB = tb_dualB(d);
+  duB.A = L.G1; duB.W = w1t; duB.R = gy; duB.C = gx;
+  duB.Bm = x; duB.Dpart = L.cpart1;
+  if (gemm_dual_eligible(dt, duB)) {
+    CTN_HIP(launch_gemm_dual(duB, s));
+  } else {
+    GemmRows gb{};
+    gb.g = rg; gb.Kred = d->H; gb.Nout = d->B; gb.norm = d->norm_type;
+    gb.A = L.G1; gb.lda = d->H;
+    gb.W = w1t; gb.ldw = d->H;
+    gb.epi = EPI_RESID; gb.R = gy; gb.ldr = d->B;
+    gb.C = gx; gb.ldc = d->B;
+    CTN_HIP(launch_gemm_rows(dt, gb, s));
+    GemmCols c1{};
+    c1.g = rg; c1.P = d->H; c1.Q = d->B;
+    c1.A = L.G1; c1.lda = d->H;
+    c1.B = x; c1.ldb = d->B;
+    c1.Cpart = L.cpart1; c1.nchunks = L.chunks1;
+    CTN_HIP(launch_gemm_cols(dt, c1, s));
+  }
   // (g) all parameter-gradient partial sums
   const int dwb = dw_blocks(da), dws = dw_col_stride(da);
   const int HB = d->H * d->B, H = d->H;

@@ -76,6 +76,33 @@ struct GemmCols {
 int gemm_cols_default_chunks(const GemmCols& p);
 hipError_t launch_gemm_cols(DType dt, const GemmCols& p, hipStream_t s);
 
+// ---- dual GEMM (ctn_gemm_dual.hip): a row GEMM and the weight gradient that shares
+// its A stream, in one pass:  C[r][n] = sum_k A[r][k] W[n][k] (+ EPI_RESID / EPI_NORM_BWD
+// epilogue, fields as GemmRows) and Dpart[range][k][n] = sum_{r in range} A[r][k] op(Bm[r][n]).
+struct GemmDual {
+  Rows g;
+  int Kred, Nout;
+  const void* A; int lda;
+  const void* W; int ldw;
+  int epi = EPI_RESID;
+  void* C; int ldc;
+  const void* R = nullptr; int ldr = 0;
+  const float* alpha = nullptr;
+  const float2* stats = nullptr;
+  const float* gamma = nullptr;
+  int norm = 0;
+  double2* grp_slab = nullptr;
+  const void* Bm; int ldb;
+  RowOp bop;                   // OP_PLAIN or OP_PRELU_NORM with final statistics
+  float* Dpart;                // [gemm_dual_ranges][Kred][Nout]
+};
+bool gemm_dual_eligible(DType dt, const GemmDual& p);
+int gemm_dual_ranges(const GemmDual& p);
+int gemm_dual_group_parts(const GemmDual& p);
+StatFold gemm_dual_stat_fold(const GemmDual& p, const double2* slab, double cnt, float eps, int mode,
+                             float2* out);
+hipError_t launch_gemm_dual(const GemmDual& p, hipStream_t s);
+
 // ---- statistics ------------------------------------------------------------
 // slab: [G][nparts] double2 partials -> out[G] float2
 //   mode 0: (mean, rstd) with biased variance, eps inside the sqrt
