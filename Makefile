@@ -36,7 +36,7 @@ build/ws_bench_%: tools/microbench/ws_bench.hip $(PKG)/csrc/ctn_gemm_ws.hip $(HD
 .PHONY: microbench
 
 # dual-GEMM bound-finding microbenchmarks: build/dual_bench_<bits>
-DU_EXPS := 0 1 2 3 4 8 12 16 32 64 18
+DU_EXPS := 0 1 4 8 12 32
 dualbench: $(patsubst %,build/dual_bench_%,$(DU_EXPS))
 build/dual_bench_%: tools/microbench/dual_bench.hip $(PKG)/csrc/ctn_gemm_dual.hip $(HDR)
 	@mkdir -p build

@@ -49,9 +49,14 @@ def kernel_bytes(kind, M, K, cfg, s=2):
         return rows * (B + H) * s + B * H * s
     if kind == TIMER_DW_FWD:       # h1[H] in, d[H] out
         return rows * 2 * H * s
-    if kind == TIMER_GEMM_BWD_A:   # gy[B] in, d[H] in, g[H] out, W2t once
-        return rows * (B + 2 * H) * s + B * H * s
+    if kind == TIMER_GEMM_BWD_A:   # gy[B] in, d[H] in, g[H] out, W2t once (+ dW2 fp32 once: dual kernel)
+        return rows * (B + 2 * H) * s + B * H * s + (B * H * 4 if dual_pair_a() else 0)
     raise ValueError(kind)
+
+
+def dual_pair_a():
+    """Pair A of the dual GEMM (ctn_gemm_dual.hip) is on unless CTN_GEMM_DUAL clears bit 0."""
+    return bool(int(os.environ.get("CTN_GEMM_DUAL", "1")) & 1)
 
 
 def step_alg_bytes(M, K, T, cfg, s=2):
@@ -198,7 +203,9 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": {1: "gemm_rows fwd 1x1 B->H (PReLU-stats epilogue)",
                                     2: "dw_fwd (norm1+depthwise+stats)",
-                                    3: "gemm_rows bwd g_n2 = gy.W2 (norm-backward epilogue)"}[args.timer_kind],
+                                    3: ("gemm_dual bwd g_n2 = gy.W2 (norm-backward epilogue) + dW2 = gy^T.n2"
+                                        if dual_pair_a() else
+                                        "gemm_rows bwd g_n2 = gy.W2 (norm-backward epilogue)")}[args.timer_kind],
                          "launches": nl.value, "mean_ms": round(mean_ms, 4), "bytes_per_launch": kb},
             "step_model": {"alg_bytes_GB": round(step_alg_bytes(M, K, T, cfg, s) / 1e9, 3),
                            "alg_GBps": round(step_alg_bytes(M, K, T, cfg, s) / (ms * 1e-3) / 1e9, 1),

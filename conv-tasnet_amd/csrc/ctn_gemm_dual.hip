@@ -37,12 +37,22 @@ typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 constexpr int DU_WV = 8, DU_NT = 512, DU_TM = 32, DU_GRID = 256;
+constexpr int DU_MMAX = 512;   // utterances whose gLN statistics a workgroup holds in LDS
 
 // Bound-finding experiments only (tools/microbench/dual_bench.hip): bit 0 drops the
 // row-part stores, 1 the A loads, 2 the row-part MFMAs, 3 the column part (reads and
 // MFMAs), 4 the Bm loads, 5 fences the epilogue off the MFMAs, 6 drops the LDS staging.
 #ifndef CTN_DU_EXP
 #define CTN_DU_EXP 0
+#endif
+// cLN per-row statistics: 1 = a 4-byte LDS-DMA per wave and tile into a per-wave ring
+// (measured racy on gfx950: run-to-run different norm-2 sums), 0 = plain loads from
+// L2 at the point of use (the default; deterministic).
+#ifndef CTN_DU_DA
+#define CTN_DU_DA 4   // LDS ring depth of the (256 -> 512, norm-backward) pair
+#endif
+#ifndef CTN_DU_CST_DMA
+#define CTN_DU_CST_DMA 0
 #endif
 
 // LDS images (byte offsets), all checked conflict-free (bank model of
@@ -105,28 +115,95 @@ template <int NV> CTN_DEV void du_bstore(rsrc_t r, uint32_t voff, int soff, cons
   }
 }
 
-// KB: Kred / 32; NSB: slice width / 16; NBW: 16-channel output blocks per wave (row part)
-template <int KB, int NSB, int NBW, int EPI, int OPB, int NK>
+// LDS-DMA (buffer_load ... lds) of one 16-byte (4-byte) piece per lane into the LDS
+// block at the wave-uniform byte address `lds` (lane l lands at lds + 16 l).  Written
+// as inline asm so that the compiler does not see an LDS write it cannot place: it
+// would put a vmcnt(0) in front of every later LDS read it cannot prove disjoint,
+// draining the ring.  The kernel counts these loads itself (du_vmwait).
+CTN_DEV uint32_t du_ldsaddr(const char* p) {
+  return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)p);
+}
+CTN_DEV void du_dma16(rsrc_t r, const char* lds, uint32_t voff, int soff) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(r), "s"(du_ldsaddr(lds)), "s"(soff)
+               : "memory");
+}
+CTN_DEV void du_dma4(rsrc_t r, const char* lds, uint32_t voff, int soff) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(r), "s"(du_ldsaddr(lds)), "s"(soff)
+               : "memory");
+}
+// s_waitcnt vmcnt(n) for a wave-uniform n (clamped down: waiting for more is safe)
+CTN_DEV void du_vmwait(int n) {
+  switch (n < 0 ? 0 : n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+  }
+}
+
+// KB: Kred / 32; NSB: slice width / 16; NBW: 16-channel output blocks per wave (row
+// part); D: LDS ring depth (tiles in flight + 1).
+//
+// Every streamed operand arrives by LDS-DMA into a D-slot ring, issued D-1 tiles
+// ahead, with no VGPR-destination loads in the loop, so every wait is an explicit
+// counted vmcnt and ~(D-1) tiles (40-100 KiB) stay in flight per CU across the
+// barriers.  Per tile t (one LDS-only barrier):
+//   wait for the DMA group the iteration reads -> barrier -> store C(t-1) from LDS
+//   (whole 128-byte lines) -> DMA group t+D-1 -> [Bm transform of tile t+1 into the
+//   B image] -> MFMAs of tile t -> epilogue of tile t into the C image.
+// Operands: A ring (WS fragment image), Bm ring (plain: the B image itself; with a
+// transform: raw rows, XOR-swizzled), R ring (plain case: residual rows), per-row
+// statistics (cLN: one 256-byte copy per wave), C image (2 parities).
+template <int KB, int NSB, int NBW, int EPI, int OPB, int NK, int D>
 __global__ __launch_bounds__(DU_NT) void gemm_dual_kernel(GemmDual p) {
   constexpr int TM = DU_TM, WV = DU_WV, NT = DU_NT;
   constexpr int KR = KB * 32;          // reduction length of the row part (= D rows)
-  constexpr int CPR = KR / 8;          // 16-byte chunks per A row
-  constexpr int NA = TM * CPR / NT;    // A chunks per thread per tile
   constexpr int NS = NSB * 16;         // slice width
-  constexpr int EB = NS * TM / NT;     // Bm elements per thread per tile (8 or 4)
   constexpr int WNB = NSB / NBW;       // row-part waves per 16-row block
   constexpr int NV = NBW * 4;          // output channels per lane (row part)
   constexpr int WN = NSB / 4;          // col-part waves along n (4 n-blocks each)
-  static_assert(NA * NT == TM * CPR && NA * 16 == CPR, "A staging: 4 rows x 16 chunks per wave-instruction");
-  static_assert(EB == 8 || EB == 4, "Bm staging: 4 rows per wave");
+  constexpr bool BXF = OPB != OP_PLAIN;                 // Bm transformed in LDS
+  constexpr bool GST = NK == NORM_GLN && (BXF || EPI == EPI_NORM_BWD);   // per-utterance stats table
+  constexpr bool CST = NK == NORM_CLN && (BXF || EPI == EPI_NORM_BWD) && CTN_DU_CST_DMA;   // per-row stats by DMA
+  constexpr bool CSG = NK == NORM_CLN && (BXF || EPI == EPI_NORM_BWD) && !CTN_DU_CST_DMA;  // per-row stats from L2
+  constexpr int A_SZ = TM * KR * 2, B_SZ = TM * NS * 2;
+  constexpr int GA = A_SZ / 1024 / WV;                 // A blocks per wave per tile
+  constexpr int G = GA + 1 + (CST ? 1 : 0);            // DMA instructions per wave per tile
+  constexpr int SST = EPI == EPI_NORM_BWD ? 1 : 0;     // statistics stores per wave per tile
+  constexpr int OFF_B = D * A_SZ;                      // Bm ring (raw rows or B image)
+  constexpr int OFF_R = OFF_B + D * B_SZ;              // residual ring (plain case)
+  constexpr int OFF_BI = OFF_R + (BXF ? 0 : D * B_SZ); // B image, 2 parities (transform case)
+  constexpr int OFF_C = OFF_BI + (BXF ? 2 * B_SZ : 0); // C image, 2 parities
+  constexpr int OFF_ST = OFF_C + 2 * B_SZ;             // cLN row statistics ring
+  constexpr int LDS = OFF_ST + (CST ? D * WV * 256 : 0);
+  static_assert(GA * WV * 1024 == A_SZ, "A blocks split evenly over the waves");
+  static_assert(BXF ? B_SZ == WV * 1024 : 2 * B_SZ == WV * 1024, "Bm/R blocks: one per wave");
   static_assert(2 * WNB == WV, "row part: 2 row blocks x WNB waves");
   static_assert(WN >= 1 && (WV / WN) * 4 * 16 == KR, "col part: 4x4 blocks per wave cover D");
   static_assert(NV == 4 || NV == 8, "epilogue vector width");
-
-  __shared__ __attribute__((aligned(16))) char sA[2][TM * KR * 2];
-  __shared__ __attribute__((aligned(16))) char sB[2][TM * NS * 2];
-  // slice constants: column-operand gamma/beta, epilogue gamma
-  __shared__ __attribute__((aligned(16))) float sgb[3][NS];
+  static_assert(!BXF || NS == 128, "transform pass: 16 chunks per row");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+  __shared__ __attribute__((aligned(16))) char smem[LDS];   // DMA rings and images
+  // Separate arrays for what no DMA writes: the compiler then proves their reads
+  // independent of the in-flight LDS-DMA (a read it cannot separate from one gets a
+  // vmcnt(0) in front of it, draining the ring).
+  __shared__ __attribute__((aligned(16))) float sg[3 * NS];                 // gamma/beta/epilogue gamma
+  __shared__ __attribute__((aligned(16))) float2 su[GST ? DU_MMAX : 1];     // gLN utterance statistics
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
@@ -151,6 +228,7 @@ __global__ __launch_bounds__(DU_NT) void gemm_dual_kernel(GemmDual p) {
   const int Kp = p.g.Kp, Kv = p.g.K;
   const rsrc_t rA = du_rsrc(p.A, rows * p.lda * 2), rB = du_rsrc(p.Bm, rows * p.ldb * 2);
   const rsrc_t rR = du_rsrc(p.R, rows * p.ldr * 2), rC = du_rsrc(p.C, rows * p.ldc * 2);
+  const rsrc_t rS = du_rsrc(p.stats, rows * 8);
   const bf16raw* W = reinterpret_cast<const bf16raw*>(p.W);
 
   // ---- row part: wave (mbw, nbg) owns rows mbw*16.. of each tile, channels
@@ -168,10 +246,18 @@ __global__ __launch_bounds__(DU_NT) void gemm_dual_kernel(GemmDual p) {
   const float eal = EPI == EPI_NORM_BWD ? p.alpha[0] : 0.f;
   const float bal = OPB == OP_PRELU_NORM ? p.bop.alpha[0] : 0.f;
   for (int c = tid; c < NS; c += NT) {
-    sgb[0][c] = OPB != OP_PLAIN ? p.bop.gamma[n0 + c] : 0.f;
-    sgb[1][c] = OPB != OP_PLAIN ? p.bop.beta[n0 + c] : 0.f;
-    sgb[2][c] = EPI == EPI_NORM_BWD ? p.gamma[n0 + c] : 0.f;
+    sg[c] = BXF ? p.bop.gamma[n0 + c] : 0.f;
+    sg[NS + c] = BXF ? p.bop.beta[n0 + c] : 0.f;
+    sg[2 * NS + c] = EPI == EPI_NORM_BWD ? p.gamma[n0 + c] : 0.f;
   }
+  if constexpr (GST)
+    for (int m = tid; m < p.g.M; m += NT) su[m] = (BXF ? p.bop.stats : p.stats)[m];
+#pragma unroll
+  for (int nb = 0; nb < NBW; ++nb)
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) du_ready(wf[nb][kb]);
+  asm volatile("" ::"v"(eal), "v"(bal));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // nothing but the ring in flight from here
   __syncthreads();
 
   // ---- col part: wave (wp, wn) owns D blocks p in [wp*64, +64), n in [n0 + wn*64, +64)
@@ -182,19 +268,67 @@ __global__ __launch_bounds__(DU_NT) void gemm_dual_kernel(GemmDual p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) dacc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  // ---- lane-constant addresses
-  // A staging: wave w stages rows 4w..4w+3; lane: row 4w + ((l>>1)&3), chunks skc + 16j
-  const int srow = 4 * wid + ((lane >> 1) & 3), skc = 2 * ((lane >> 3) & 7) + (lane & 1);
-  const uint32_t avoff = (uint32_t)(srow * p.lda * 2 + skc * 16);
-  const int aw = du_apiece<KB>(srow, skc);                 // + j * 4096
-  // Bm staging: wave w stages rows 4w..4w+3; lane: row 4w + (l&3), EB columns at bcol
-  const int brow = 4 * wid + (lane & 3);
-  const int bcol = EB == 8 ? 16 * (lane >> 3) + 8 * ((lane >> 2) & 1) : 16 * (lane >> 4) + 4 * ((lane >> 2) & 3);
-  const uint32_t bvoff = (uint32_t)(brow * p.ldb * 2 + (n0 + bcol) * 2);
-  const int bw = du_boff(brow, bcol);
-  // row-part fragment reads: + kb * 1024
-  const int rbase = mbw * KB * 1024 + lg * 256 + ((lr ^ ((lg & 1) * 12)) << 4);
-  // col-part transposed reads, h = 0/1 (rows 8lg+4h+q): A + (i>>1)*1024 + (i&1)*512, B + j*1024
+  // ---- DMA sources (lane-constant; + tile offset in soffset)
+  // A block f = wid*GA + u = (mb, kb): lane L -> row 16mb + ((L&15) ^ 12*((L>>4)&1)), chunk 4kb + (L>>4)
+  uint32_t avo[GA];
+  int arow[GA];
+#pragma unroll
+  for (int u = 0; u < GA; ++u) {
+    const int f = wid * GA + u, mb = f / KB, kb = f % KB;
+    arow[u] = 16 * mb + ((lane & 15) ^ (((lane >> 4) & 1) * 12));
+    avo[u] = (uint32_t)(arow[u] * p.lda * 2 + (4 * kb + (lane >> 4)) * 16);
+  }
+  // Bm / R block of this wave
+  int brow;
+  uint32_t bvo;
+  bool is_r = false;
+  if constexpr (BXF) {   // raw rows: wave w -> rows 4w..4w+3, lane L -> physical chunk L&15
+    brow = 4 * wid + (lane >> 4);
+    bvo = (uint32_t)(brow * p.ldb * 2 + (n0 + 8 * ((lane & 15) ^ (brow & 15))) * 2);
+  } else if (wid < 4) {  // B image block cb = wid (du_boff is lane-linear per block)
+    const int q8 = lane >> 3;
+    brow = 4 * (q8 ^ ((q8 >> 1) & 1)) + ((lane >> 1) & 3);
+    bvo = (uint32_t)(brow * p.ldb * 2 + (n0 + 16 * wid + 8 * (lane & 1)) * 2);
+  } else {               // residual rows: block q -> rows 8q.., physical chunk L&7
+    is_r = true;
+    brow = 8 * (wid - 4) + (lane >> 3);
+    bvo = (uint32_t)(brow * p.ldr * 2 + (n0 + 8 * ((lane & 7) ^ (brow & 7))) * 2);
+  }
+  auto dma = [&](int t) __attribute__((always_inline)) {   // group of tile t -> slot t % D
+    const int slot = t % D, tk = (t * TM) % Kp;
+#pragma unroll
+    for (int u = 0; u < GA; ++u) {
+      // rows of padded frames arrive as zeros (out-of-range offset)
+      const uint32_t vo = tk + arow[u] < Kv ? avo[u] : DU_OOB;
+      du_dma16(rA, smem + slot * A_SZ + (wid * GA + u) * 1024, vo, t * TM * p.lda * 2);
+    }
+    if constexpr (BXF) {
+      du_dma16(rB, smem + OFF_B + slot * B_SZ + wid * 1024, bvo, t * TM * p.ldb * 2);
+    } else {
+      if (!is_r) du_dma16(rB, smem + OFF_B + slot * B_SZ + wid * 1024, bvo, t * TM * p.ldb * 2);
+      else du_dma16(rR, smem + OFF_R + slot * B_SZ + (wid - 4) * 1024, bvo, t * TM * p.ldr * 2);
+    }
+    if constexpr (CST) du_dma4(rS, smem + OFF_ST + (slot * WV + wid) * 256, (uint32_t)(lane * 4), t * TM * 8);
+  };
+  // vmcnt that retires DMA group tq at the top of iteration t (k = t - t0): the
+  // operations issued after it, by the fixed per-iteration order
+  // [C store (k >= 1), DMA group (G), statistics store (SST)]
+  auto ops_after = [&](int tq, int t) __attribute__((always_inline)) {
+    const int j = tq - t0, k = t - t0;
+    int n = 0, kfrom;
+    if (j <= D - 2) {
+      n = (D - 2 - j) * G;
+      kfrom = 0;
+    } else {
+      n = SST;
+      kfrom = j - D + 2;
+    }
+    for (int kk = kfrom; kk < k; ++kk) n += (kk >= 1 ? 1 : 0) + G + SST;
+    return n;
+  };
+
+  // ---- lane-constant LDS read addresses
+  const int rbase = mbw * KB * 1024 + lg * 256 + ((lr ^ ((lg & 1) * 12)) << 4);   // + kb * 1024
   const int q = lr >> 2, pp = lr & 3;
   int abase[2], bbase[2];
 #pragma unroll
@@ -204,77 +338,64 @@ __global__ __launch_bounds__(DU_NT) void gemm_dual_kernel(GemmDual p) {
                (pp & 1) * 8;
     bbase[h] = wn * 4 * 1024 + du_boff(row, 4 * pp);
   }
-  // epilogue rows: mbw*16 + lr of each tile
-  const int erow = mbw * 16 + lr;
-  const uint32_t rvoff = (uint32_t)(erow * p.ldr * 2 + colbase * 2);
-  const uint32_t cvoff = (uint32_t)(erow * p.ldc * 2 + colbase * 2);
+  const int erow = mbw * 16 + lr;                 // epilogue row of each tile
+  const int ecol = colbase - n0;                  // epilogue column inside the slice
+  // C image: row-major NS*2 bytes per row, NV-element granules XOR (row & 15)
+  const int cw = erow * NS * 2 + (((ecol / NV) ^ (erow & 15)) * NV * 2);
+  // C store pass: thread -> row tid/16, granule tid%16 (NS/16 elements)
+  constexpr int CG = NS / 16;                     // elements per store granule (8 or 4)
+  const int crow = tid >> 4, cgr = tid & 15;
+  const int cr = crow * NS * 2 + ((cgr ^ (crow & 15)) * CG * 2);
+  const uint32_t cvo = (uint32_t)(crow * p.ldc * 2 + (n0 + cgr * CG) * 2);
+  // epilogue residual / pre-activation read
+  int rdo;
+  if constexpr (BXF) rdo = erow * 256 + (((ecol >> 3) ^ (erow & 15)) << 4);                       // raw rows
+  else rdo = erow * 128 + ((((ecol >> 3) ^ (erow & 7)) << 4)) + ((ecol >> 2) & 1) * 8;          // R ring
+  // transform pass (BXF): lane -> row 4w + (l&3), physical chunk ((l>>2) + 4(l&3)) & 15
+  const int xrow = 4 * wid + (lane & 3), xp = ((lane >> 2) + 4 * (lane & 3)) & 15;
+  const int xg = xp ^ (xrow & 15);                // global chunk (channels n0 + 8xg ..)
+  const int xrd = xrow * 256 + xp * 16, xwr = du_boff(xrow, 8 * xg);
 
-  // ---- per-tile operand registers (loaded one tile ahead of their use)
-  v4u ra[NA];
-  DuVec<EB> rb;
-  float2 bst = make_float2(0.f, 0.f);
-  bool bvalid = true;
-  auto load_ab = [&](int t) __attribute__((always_inline)) {
-    const int tk = (t * TM) % Kp;   // frame of the tile's first row (tiles never straddle utterances)
-    // rows of padded frames load as zeros (out-of-range buffer offset)
-    const uint32_t vo = tk + srow < Kv ? avoff : DU_OOB;
-    const int so = t * TM * p.lda * 2;
-#pragma unroll
-    for (int j = 0; j < NA; ++j)
-      if constexpr (CTN_DU_EXP & 2) ra[j] = v4u{vo, (uint32_t)so, 0u, 0u};
-      else ra[j] = __builtin_amdgcn_raw_buffer_load_b128(rA, vo + j * 256, so, 0);
-    if constexpr (CTN_DU_EXP & 16) { for (int e = 0; e < EB / 2; ++e) rb.w[e] = bvoff + t; }
-    else rb = du_bload<EB>(rB, bvoff, t * TM * p.ldb * 2);
-    if constexpr (OPB != OP_PLAIN) bst = p.bop.stats[stat_index<NK>(t * TM + brow, Kp)];
-    if constexpr (OPB != OP_PLAIN && NK == NORM_CLN) bvalid = tk + brow < Kv;
-  };
-  // Bm transform: padded frames are zeroed only under cLN (their per-row statistics are
-  // not finite); otherwise A is zero there and the D products vanish
-  auto stage = [&](auto le1, int buf) __attribute__((always_inline)) {
-    constexpr bool LE1 = decltype(le1)::value;
-#pragma unroll
-    for (int j = 0; j < NA; ++j)
-      if constexpr (!(CTN_DU_EXP & 64)) stg16(sA[buf] + aw + j * 4096, ra[j]);
-    uint32_t w[EB / 2];
-#pragma unroll
-    for (int e = 0; e < EB / 2; ++e) w[e] = rb.w[e];
-    if constexpr (OPB != OP_PLAIN) {
-      const f32x2_t m2 = {bst.x, bst.x};
-#pragma unroll
-      for (int e = 0; e < EB / 2; ++e) {
-        const float2 g = *reinterpret_cast<const float2*>(&sgb[0][bcol + 2 * e]);
-        const float2 bt = *reinterpret_cast<const float2*>(&sgb[1][bcol + 2 * e]);
-        f32x2_t x = {__uint_as_float(w[e] << 16), __uint_as_float(w[e] & 0xffff0000u)};
-        if constexpr (OPB == OP_PRELU_NORM) x = prelu2<LE1>(x, bal);
-        x = pfma(x - m2, f32x2_t{bst.y * g.x, bst.y * g.y}, f32x2_t{bt.x, bt.y});
-        w[e] = pk_bf16(x[0], x[1]);
-        if constexpr (NK == NORM_CLN) w[e] = bvalid ? w[e] : 0u;
-      }
-    }
-    if constexpr (CTN_DU_EXP & 64) { asm volatile("" ::"v"(w[0]), "v"(w[1])); }
-    else if constexpr (EB == 8) stg16(sB[buf] + bw, v4u{w[0], w[1], w[2], w[3]});
-    else *reinterpret_cast<uint2*>(sB[buf] + bw) = make_uint2(w[0], w[1]);
-  };
-
-  // ---- row epilogue operand (residual or pre-activation), one tile ahead
-  DuVec<NV> rn;
-  float2 est = make_float2(0.f, 0.f);
-  auto load_r = [&](int t) __attribute__((always_inline)) {
-    rn = du_bload<NV>(rR, rvoff, t * TM * p.ldr * 2);
-    if constexpr (EPI == EPI_NORM_BWD) est = p.stats[stat_index<NK>(t * TM + erow, Kp)];
-  };
-
-  // gLN run partials (WsRuns layout with waves = S * WV: slot (sl*WV + wid)); the running
-  // sum of the current utterance is stored every tile (the last store of a run is its total)
   double run_s = 0.0, run_q = 0.0;
   const int tpu = Kp / TM, m0 = t0 / tpu;
   int run_m = m0;
   const int kmax = ws_runs_kmax(ntile, nr, tpu);
   double2* run_slab = p.grp_slab + (((size_t)rr * S + sl) * WV + wid) * kmax;
 
-  auto compute = [&](int buf, f32x4_t (&acc)[NBW]) __attribute__((always_inline)) {
-    const char* a = sA[buf];
-    const char* bsl = sB[buf];
+  // statistics of frame row r (tile-relative rt) of tile t whose ring slot is `slot`
+  auto row_stat = [&](int t, int slot, int rt) __attribute__((always_inline)) {
+    if constexpr (GST) return su[(t * TM) / Kp];
+    else if constexpr (CSG) return p.stats[t * TM + rt];
+    else return *reinterpret_cast<const float2*>(smem + OFF_ST + (slot * WV + wid) * 256 + rt * 8);
+  };
+
+  auto transform = [&](auto le1, int t) __attribute__((always_inline)) {   // raw Bm(t) -> B image (t & 1)
+    constexpr bool LE1 = decltype(le1)::value;
+    const int slot = t % D;
+    v4u v = *reinterpret_cast<const v4u*>(smem + OFF_B + slot * B_SZ + xrd);
+    const float2 st = row_stat(t, slot, xrow);
+    const float4 g0 = *reinterpret_cast<const float4*>(&sg[8 * xg]), g1 = *reinterpret_cast<const float4*>(&sg[8 * xg + 4]);
+    const float4 b0 = *reinterpret_cast<const float4*>(&sg[NS + 8 * xg]), b1 = *reinterpret_cast<const float4*>(&sg[NS + 8 * xg + 4]);
+    const float gv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+    const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    const f32x2_t m2 = {st.x, st.x};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      f32x2_t x = {__uint_as_float(v[e] << 16), __uint_as_float(v[e] & 0xffff0000u)};
+      if constexpr (OPB == OP_PRELU_NORM) x = prelu2<LE1>(x, bal);
+      x = pfma(x - m2, f32x2_t{st.y * gv[2 * e], st.y * gv[2 * e + 1]}, f32x2_t{bv[2 * e], bv[2 * e + 1]});
+      v[e] = pk_bf16(x[0], x[1]);
+    }
+    // cLN: padded frames' row statistics are not finite; gLN: A is zero there
+    if constexpr (NK == NORM_CLN) {
+      if ((t * TM) % Kp + xrow >= Kv) v = v4u{0u, 0u, 0u, 0u};
+    }
+    stg16(smem + OFF_BI + (t & 1) * B_SZ + xwr, v);
+  };
+
+  auto compute = [&](int t, f32x4_t (&acc)[NBW]) __attribute__((always_inline)) {
+    const char* a = smem + (t % D) * A_SZ;
+    const char* bsl = BXF ? smem + OFF_BI + (t & 1) * B_SZ : smem + OFF_B + (t % D) * B_SZ;
 #pragma unroll
     for (int nb = 0; nb < NBW; ++nb) acc[nb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -306,34 +427,47 @@ __global__ __launch_bounds__(DU_NT) void gemm_dual_kernel(GemmDual p) {
         dacc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], dacc[i][j], 0, 0, 0);
   };
 
-  // row epilogue of tile t: lane holds row t*TM + erow, channels colbase..+NV
+  // row epilogue of tile t: lane holds row t*TM + erow, channels colbase..+NV -> C image (t & 1)
   auto epilogue = [&](auto le1, int t, const f32x4_t (&acc)[NBW]) __attribute__((always_inline)) {
     constexpr bool LE1 = decltype(le1)::value;
+    const int slot = t % D;
     f32x2_t v2[NV / 2];
 #pragma unroll
     for (int nb = 0; nb < NBW; ++nb) {
       v2[2 * nb] = f32x2_t{acc[nb][0], acc[nb][1]};
       v2[2 * nb + 1] = f32x2_t{acc[nb][2], acc[nb][3]};
     }
+    uint32_t rw[NV / 2];
+    if constexpr (NV == 8) {
+      const v4u r4 = *reinterpret_cast<const v4u*>(smem + (BXF ? OFF_B : OFF_R) + slot * B_SZ + rdo);
+      rw[0] = r4[0]; rw[1] = r4[1]; rw[2] = r4[2]; rw[3] = r4[3];
+    } else {
+      const uint2 r2 = *reinterpret_cast<const uint2*>(smem + (BXF ? OFF_B : OFF_R) + slot * B_SZ + rdo);
+      rw[0] = r2.x; rw[1] = r2.y;
+    }
     f32x2_t s2 = {0.f, 0.f}, q2 = {0.f, 0.f};
     if constexpr (EPI == EPI_RESID) {
 #pragma unroll
-      for (int c = 0; c < NV / 2; ++c)
-        v2[c] += f32x2_t{__uint_as_float(rn.w[c] << 16), __uint_as_float(rn.w[c] & 0xffff0000u)};
+      for (int c = 0; c < NV / 2; ++c) v2[c] += f32x2_t{__uint_as_float(rw[c] << 16), __uint_as_float(rw[c] & 0xffff0000u)};
     } else {
+      const float2 est = row_stat(t, slot, erow);
       const f32x2_t rs = {est.y, est.y}, ms = {-est.x * est.y, -est.x * est.y};
 #pragma unroll
       for (int c = 0; c < NV / 2; ++c) {
-        const float2 g = *reinterpret_cast<const float2*>(&sgb[2][colbase - n0 + 2 * c]);
-        const f32x2_t x = {__uint_as_float(rn.w[c] << 16), __uint_as_float(rn.w[c] & 0xffff0000u)};
+        const float2 g = *reinterpret_cast<const float2*>(&sg[2 * NS + ecol + 2 * c]);
+        const f32x2_t x = {__uint_as_float(rw[c] << 16), __uint_as_float(rw[c] & 0xffff0000u)};
         const f32x2_t ah = pfma(prelu2<LE1>(x, eal), rs, ms);   // hat a
         const f32x2_t ga = v2[c] * f32x2_t{g.x, g.y};
         s2 += ga;
         q2 = pfma(ga, ah, q2);
       }
     }
-    if constexpr (!(CTN_DU_EXP & 1)) du_bstore<NV>(rC, cvoff, t * TM * p.ldc * 2, v2);
-    else asm volatile("" ::"v"(v2[0]));
+    char* cdst = smem + OFF_C + (t & 1) * B_SZ + cw;
+    if constexpr (NV == 8)
+      stg16(cdst, v4u{pk_bf16(v2[0][0], v2[0][1]), pk_bf16(v2[1][0], v2[1][1]), pk_bf16(v2[2][0], v2[2][1]),
+                      pk_bf16(v2[3][0], v2[3][1])});
+    else
+      *reinterpret_cast<uint2*>(cdst) = make_uint2(pk_bf16(v2[0][0], v2[0][1]), pk_bf16(v2[1][0], v2[1][1]));
     if constexpr (EPI == EPI_NORM_BWD) {
       if constexpr (NK == NORM_GLN) {
         const float s = wave_sum_dpp(s2[0] + s2[1]), ss = wave_sum_dpp(q2[0] + q2[1]);
@@ -344,7 +478,6 @@ __global__ __launch_bounds__(DU_NT) void gemm_dual_kernel(GemmDual p) {
         run_m = m;
         run_slab[m - m0] = make_double2(run_s, run_q);
       } else {
-        // per-row partial over the wave's channels: reduce across the 4 lane groups
         float s = s2[0] + s2[1], ss = q2[0] + q2[1];
         s += __shfl_xor(s, 16, 64); ss += __shfl_xor(ss, 16, 64);
         s += __shfl_xor(s, 32, 64); ss += __shfl_xor(ss, 32, 64);
@@ -353,39 +486,45 @@ __global__ __launch_bounds__(DU_NT) void gemm_dual_kernel(GemmDual p) {
     }
   };
 
-#pragma unroll
-  for (int nb = 0; nb < NBW; ++nb)
-#pragma unroll
-    for (int kb = 0; kb < KB; ++kb) du_ready(wf[nb][kb]);
-  asm volatile("" ::"v"(eal), "v"(bal));
+  // C(t) from its LDS image to global memory: every wave stores whole rows
+  auto store_c = [&](int t) __attribute__((always_inline)) {
+    const char* src = smem + OFF_C + (t & 1) * B_SZ + cr;
+    const uint32_t vo = cvo + (uint32_t)(t * TM * p.ldc * 2);   // soffset 0: see du_bstore
+    if constexpr (CG == 8) {
+      const v4u v = *reinterpret_cast<const v4u*>(src);
+      if constexpr (!(CTN_DU_EXP & 1)) __builtin_amdgcn_raw_buffer_store_b128(v, rC, vo, 0, 0);
+      else asm volatile("" ::"v"(v));
+    } else {
+      typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+      const v2u v = *reinterpret_cast<const v2u*>(src);
+      if constexpr (!(CTN_DU_EXP & 1)) __builtin_amdgcn_raw_buffer_store_b64(v, rC, vo, 0, 0);
+      else asm volatile("" ::"v"(v));
+    }
+  };
 
-  // Pipeline (unrolled by two: static LDS buffer parity): after one LDS-only barrier,
-  // the MFMAs of tile t, its epilogue, the staging of tile t+1 (registers loaded one
-  // iteration earlier) and the loads of tile t+2.  No scheduling fence: the epilogue
-  // and staging VALU work interleaves with the column part's MFMAs.
   auto clampt = [&](int t) __attribute__((always_inline)) { return t < t1 ? t : t1 - 1; };
   auto run = [&](auto le1) __attribute__((always_inline)) {
     f32x4_t acc[NBW];
-    load_ab(t0);
-    load_r(t0);
-    stage(le1, 0);
-    load_ab(clampt(t0 + 1));
-    auto step = [&](int t, auto par) __attribute__((always_inline)) {
-      constexpr int P = decltype(par)::value;
+    for (int i = 0; i < D - 1; ++i) dma(clampt(t0 + i));
+    for (int t = t0; t < t1; ++t) {
+      // BXF: the transform reads raw Bm of tile t+1 this iteration, so wait for its group
+      const int tq = BXF ? t + 1 : t;
+      du_vmwait(ops_after(tq, t));
+      if (BXF && t == t0) {   // the first tile's raw rows: transform them before everything
+        lds_barrier();
+        transform(le1, t0);
+      }
       lds_barrier();
-      compute(P, acc);
+      if (t > t0) store_c(t - 1);
+      dma(clampt(t + D - 1));
+      if constexpr (BXF) transform(le1, clampt(t + 1));
+      compute(t, acc);
       if constexpr (CTN_DU_EXP & 32) __builtin_amdgcn_sched_barrier(0);
       epilogue(le1, t, acc);
-      load_r(clampt(t + 1));
-      stage(le1, 1 - P);
-      load_ab(clampt(t + 2));
-    };
-    int t = t0;
-    for (; t + 1 < t1; t += 2) {
-      step(t, std::integral_constant<int, 0>{});
-      step(t + 1, std::integral_constant<int, 1>{});
     }
-    if (t < t1) step(t, std::integral_constant<int, 0>{});
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may land after the workgroup ends
+    lds_barrier();
+    store_c(t1 - 1);
   };
   if (t0 < t1) {
     constexpr bool PR = OPB == OP_PRELU_NORM || EPI == EPI_NORM_BWD;
@@ -409,12 +548,15 @@ __global__ __launch_bounds__(DU_NT) void gemm_dual_kernel(GemmDual p) {
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-// CTN_GEMM_DUAL=1 selects the dual kernels, 0 the four-kernel path (row GEMM + column
-// GEMM twice); read on every query so a process can compare both (tests/test_gpu_tblock.py).
-// Default: off until it measures faster than the four kernels.
-static bool dual_enabled() {
+// CTN_GEMM_DUAL=<mask> selects the dual kernels per pair: bit 0 the (256 -> 512,
+// norm-backward) pair "A" (gy.W2 + dW2), bit 1 the (512 -> 256, residual) pair "B"
+// (gh1.W1 + dW1); cleared bits run the row GEMM + column GEMM kernels.  Read on every
+// query so a process can compare both paths (tests/test_gpu_tblock.py).  Default 1:
+// pair A measures 109 us against 62 + 60 us for its two kernels; pair B 103 us against
+// 49 + 45 us (tools/microbench/dual_bench.hip), so B stays on the two kernels.
+static int dual_mask() {
   const char* e = getenv("CTN_GEMM_DUAL");
-  return e && atoi(e) == 1;
+  return e ? atoi(e) : 1;
 }
 
 // (Kred, Nout) -> (KB, NSB, NBW); S = 4 slices
@@ -426,13 +568,16 @@ static bool dual_shape(int Kred, int Nout, int* kb, int* nsb, int* nbw) {
 
 bool gemm_dual_eligible(DType dt, const GemmDual& p) {
   int kb, nsb, nbw;
-  if (dt != BF16 || !dual_enabled() || !dual_shape(p.Kred, p.Nout, &kb, &nsb, &nbw)) return false;
+  if (dt != BF16 || !dual_shape(p.Kred, p.Nout, &kb, &nsb, &nbw)) return false;
   const bool pairA = p.Kred == 256 && p.epi == EPI_NORM_BWD && p.bop.kind == OP_PRELU_NORM;
   const bool pairB = p.Kred == 512 && p.epi == EPI_RESID && p.bop.kind == OP_PLAIN;
-  if (!pairA && !pairB) return false;
+  const int mask = dual_mask();
+  if (!(pairA && (mask & 1)) && !(pairB && (mask & 2))) return false;
   if (p.bop.kind != OP_PLAIN && p.bop.fold.slab) return false;   // needs final statistics
   if (p.g.Kp % DU_TM || p.lda % 8 || p.ldw % 8 || p.ldc % 8 || p.ldr % 8 || p.ldb % 8) return false;
-  if (p.g.rows() / DU_TM < 1 || p.g.rows() >= (1L << 31)) return false;
+  if (p.g.rows() / DU_TM < 1 || p.g.rows() * (p.Kred > p.Nout ? p.Kred : p.Nout) * 2 >= (1L << 31)) return false;
+  if (p.norm == NORM_GLN && p.g.M > DU_MMAX) return false;
+  if (pairA && p.stats != p.bop.stats) return false;   // one statistics table serves both
   return true;
 }
 
@@ -485,9 +630,9 @@ template <int NK>
 static hipError_t dual_launch_nk(const GemmDual& p, hipStream_t s) {
   const dim3 grid(gemm_dual_ranges(p) * dual_slices(p));
   if (p.Kred == 256 && p.epi == EPI_NORM_BWD && p.bop.kind == OP_PRELU_NORM)
-    hipLaunchKernelGGL((gemm_dual_kernel<8, 8, 2, EPI_NORM_BWD, OP_PRELU_NORM, NK>), grid, dim3(DU_NT), 0, s, p);
+    hipLaunchKernelGGL((gemm_dual_kernel<8, 8, 2, EPI_NORM_BWD, OP_PRELU_NORM, NK, CTN_DU_DA>), grid, dim3(DU_NT), 0, s, p);
   else if (p.Kred == 512 && p.epi == EPI_RESID && p.bop.kind == OP_PLAIN)
-    hipLaunchKernelGGL((gemm_dual_kernel<16, 4, 1, EPI_RESID, OP_PLAIN, NORM_GLN>), grid, dim3(DU_NT), 0, s, p);
+    hipLaunchKernelGGL((gemm_dual_kernel<16, 4, 1, EPI_RESID, OP_PLAIN, NORM_GLN, 3>), grid, dim3(DU_NT), 0, s, p);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();

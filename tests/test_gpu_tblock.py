@@ -153,7 +153,7 @@ def test_dual_gemm_matches_four_kernel_path(d, causal, norm, monkeypatch):
     x = torch.randn(M, B, K)
     G = torch.randn(M, B, K)
     outs = []
-    for flag in ("0", "1"):
+    for flag in ("0", "3"):   # four-kernel path vs both dual pairs
         monkeypatch.setenv("CTN_GEMM_DUAL", flag)
         outs.append(run_block(x, params, 3, d, causal, norm, G, torch.bfloat16)[:3])
     (y0, gx0, gp0), (y1, gx1, gp1) = outs
@@ -163,3 +163,25 @@ def test_dual_gemm_matches_four_kernel_path(d, causal, norm, monkeypatch):
     assert rel(gx1, gx0) < 2e-3
     for (n, e), a, b in zip(errs.items(), gp1, gp0):
         assert e < 5e-3 or (a.numel() == 1 and abs(float(a - b)) < 1e-2 * (1 + abs(float(b)))), (n, errs)
+
+
+@pytest.mark.parametrize("dual", ["0", "3"])
+@pytest.mark.parametrize("d,causal,norm", [(2, 0, "gLN"), (32, 1, "cLN"), (2, 0, "cLN")])
+def test_backward_bitwise_deterministic(d, causal, norm, dual, monkeypatch):
+    """Every statistic and gradient partial is combined in a fixed order:
+    repeated runs on identical inputs give bit-identical outputs and gradients."""
+    monkeypatch.setenv("CTN_GEMM_DUAL", dual)
+    torch.manual_seed(0)
+    params = _paper_block(5, causal=bool(causal), norm=norm)
+    M, B, K = 3, 256, 1000
+    x = torch.randn(M, B, K)
+    G = torch.randn(M, B, K)
+    runs = [run_block(x, params, 3, d, causal, norm, G, torch.bfloat16)[:3] for _ in range(3)]
+    ref = run_block(x, params, 3, d, causal, norm, G, torch.float32)[:3]
+    y0, gx0, gp0 = runs[0]
+    print("vs fp32:", "gx", rel(gx0, ref[1]), {n: rel(a, b) for n, a, b in zip(_names(causal), gp0, ref[2])})
+    for y, gx, gp in runs[1:]:
+        assert torch.equal(y0, y)
+        assert torch.equal(gx0, gx), rel(gx, gx0)
+        for n, a, b in zip(_names(causal), gp, gp0):
+            assert torch.equal(a, b), (n, rel(a, b))
