@@ -36,7 +36,7 @@ build/ws_bench_%: tools/microbench/ws_bench.hip $(PKG)/csrc/ctn_gemm_ws.hip $(HD
 .PHONY: microbench
 
 # dual-GEMM bound-finding microbenchmarks: build/dual_bench_<bits>
-DU_EXPS := 0 1 4 8 12 32
+DU_EXPS := 0 12 13 14 28 76 92 94 222
 dualbench: $(patsubst %,build/dual_bench_%,$(DU_EXPS))
 build/dual_bench_%: tools/microbench/dual_bench.hip $(PKG)/csrc/ctn_gemm_dual.hip $(HDR)
 	@mkdir -p build

@@ -295,6 +295,7 @@ __global__ __launch_bounds__(DU_NT) void gemm_dual_kernel(GemmDual p) {
     bvo = (uint32_t)(brow * p.ldr * 2 + (n0 + 8 * ((lane & 7) ^ (brow & 7))) * 2);
   }
   auto dma = [&](int t) __attribute__((always_inline)) {   // group of tile t -> slot t % D
+    if constexpr (CTN_DU_EXP & 2) return;
     const int slot = t % D, tk = (t * TM) % Kp;
 #pragma unroll
     for (int u = 0; u < GA; ++u) {
@@ -371,6 +372,7 @@ __global__ __launch_bounds__(DU_NT) void gemm_dual_kernel(GemmDual p) {
 
   auto transform = [&](auto le1, int t) __attribute__((always_inline)) {   // raw Bm(t) -> B image (t & 1)
     constexpr bool LE1 = decltype(le1)::value;
+    if constexpr (CTN_DU_EXP & 16) return;
     const int slot = t % D;
     v4u v = *reinterpret_cast<const v4u*>(smem + OFF_B + slot * B_SZ + xrd);
     const float2 st = row_stat(t, slot, xrow);
@@ -430,6 +432,10 @@ __global__ __launch_bounds__(DU_NT) void gemm_dual_kernel(GemmDual p) {
   // row epilogue of tile t: lane holds row t*TM + erow, channels colbase..+NV -> C image (t & 1)
   auto epilogue = [&](auto le1, int t, const f32x4_t (&acc)[NBW]) __attribute__((always_inline)) {
     constexpr bool LE1 = decltype(le1)::value;
+    if constexpr (CTN_DU_EXP & 64) {
+      *reinterpret_cast<float*>(smem + OFF_C + (t & 1) * B_SZ + cw) = acc[0][0];
+      return;
+    }
     const int slot = t % D;
     f32x2_t v2[NV / 2];
 #pragma unroll
@@ -509,7 +515,7 @@ __global__ __launch_bounds__(DU_NT) void gemm_dual_kernel(GemmDual p) {
     for (int t = t0; t < t1; ++t) {
       // BXF: the transform reads raw Bm of tile t+1 this iteration, so wait for its group
       const int tq = BXF ? t + 1 : t;
-      du_vmwait(ops_after(tq, t));
+      if constexpr (!(CTN_DU_EXP & 128)) du_vmwait(ops_after(tq, t));
       if (BXF && t == t0) {   // the first tile's raw rows: transform them before everything
         lds_barrier();
         transform(le1, t0);

@@ -31,7 +31,10 @@ namespace ctn {
 typedef short bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
-constexpr int WS_WAVES = 8, WS_TM = 16, WS_GRID = 256;
+#ifndef CTN_WS_GRID
+#define CTN_WS_GRID 256
+#endif
+constexpr int WS_WAVES = 8, WS_TM = 16, WS_GRID = CTN_WS_GRID;
 constexpr int WS_FOLD_MAX = 512;   // utterances whose gLN operand stats a workgroup holds in LDS
 
 // Bound-finding experiments only (tools/microbench): bit 0 drops the output
