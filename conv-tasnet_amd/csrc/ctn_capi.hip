@@ -200,6 +200,32 @@ GemmDual tb_dualB(const ctn_tblock_desc* d) {
   g.epi = EPI_RESID;
   return g;
 }
+// backward gx = op(g) . W1 + gy; op = norm-1/PReLU-1 backward (fused path) or plain
+GemmRows tb_gemmB(const ctn_tblock_desc* d, bool fused) {
+  GemmRows g{};
+  g.g = Rows{d->M, d->K, d->Kp};
+  g.Kred = d->H; g.Nout = d->B; g.norm = d->norm_type;
+  g.lda = d->H; g.ldw = d->H; g.epi = EPI_RESID; g.ldr = d->B; g.ldc = d->B;
+  if (fused) {
+    g.aop.kind = OP_NORM1_BWD; g.aop.norm = d->norm_type;
+  }
+  return g;
+}
+// The norm-1/PReLU-1 backward runs inside the first 1x1's two gradient GEMMs (bf16,
+// gLN, weight-stationary data-gradient kernel, dual pair B off); else norm1_bwd_kernel.
+// CTN_FUSE_N1=0 keeps the separate kernel (read on every query, so a process can
+// compare both paths: tests/test_gpu_tblock.py).
+bool tb_fused_n1(const ctn_tblock_desc* d) {
+  const char* e = getenv("CTN_FUSE_N1");
+  if (e && atoi(e) == 0) return false;
+  if (d->dtype != CTN_DTYPE_BF16 || d->norm_type != CTN_NORM_GLN) return false;
+  if (gemm_dual_eligible(BF16, tb_dualB(d))) return false;
+  GemmRows g = tb_gemmB(d, true);
+  static const float dummy[2] = {0.f, 0.f};   // eligibility only checks presence
+  g.aop.aux = dummy; g.aop.apart = const_cast<float*>(dummy); g.aop.aout = const_cast<float*>(dummy);
+  g.aop.stats = reinterpret_cast<const float2*>(dummy); g.aop.sums = reinterpret_cast<const float2*>(dummy);
+  return gemm_ws_eligible(BF16, g);
+}
 DType tb_dt(const ctn_tblock_desc* d) { return d->dtype == CTN_DTYPE_BF16 ? BF16 : F32; }
 
 TbLayout tb_layout(const ctn_tblock_desc* d, int backward, void* ws) {
@@ -237,7 +263,8 @@ TbLayout tb_layout(const ctn_tblock_desc* d, int backward, void* ws) {
     L.partsD = dw_parts_per_group(da);
     L.slabD = c.take<double2>((size_t)G * L.partsD * sizeof(double2));
     L.colD = c.take<float>((size_t)dw_blocks(da) * dw_col_stride(da) * sizeof(float));
-    L.alphaSlab = c.take<float>((size_t)ew_blocks(da) * sizeof(float));
+    const int na = tb_fused_n1(d) ? gemm_ws_grid(tb_gemmB(d, true)) : ew_blocks(da);
+    L.alphaSlab = c.take<float>((size_t)(na > ew_blocks(da) ? na : ew_blocks(da)) * sizeof(float));
     L.sums1 = c.take<float2>((size_t)G * sizeof(float2));
     L.sums2 = c.take<float2>((size_t)G * sizeof(float2));
     GemmCols gc{};
@@ -411,34 +438,57 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
     da.f_sm2 = dualA ? gemm_dual_stat_fold(duA, L.slabA, cnt, 0.f, 1, nullptr)
                      : gemm_rows_stat_fold(dt, ga, L.slabA, cnt, 0.f, 1, nullptr);
   CTN_HIP(launch_dw_bwd(dt, da, s));
-  if (!fold) CTN_HIP(launch_stats_finalize(L.slabD, G, L.partsD, cnt, 1, 0.f, L.sums1, s));
-  // (d) norm1 backward finish + PReLU1 backward -> G1 = dL/dh1
-  DwArgs de = da;
-  de.ga2 = L.G2; de.sm1 = L.sums1; de.gh1_out = L.G1; de.alpha_slab = L.alphaSlab;
-  de.f_sm2 = StatFold{};
-  if (fold) de.f_sm1 = StatFold{L.slabD, L.partsD, cnt, 0.f, 1, nullptr};
-  CTN_HIP(launch_norm1_bwd(dt, de, s));
-  // (e) gx = gh1 . W1 + gy
-  // (f) dW1 = gh1^T . x                          — one dual-GEMM pass when eligible
-  GemmDual duB = tb_dualB(d);
-  duB.A = L.G1; duB.W = w1t; duB.R = gy; duB.C = gx;
-  duB.Bm = x; duB.Dpart = L.cpart1;
-  if (gemm_dual_eligible(dt, duB)) {
-    CTN_HIP(launch_gemm_dual(duB, s));
-  } else {
-    GemmRows gb{};
-    gb.g = rg; gb.Kred = d->H; gb.Nout = d->B; gb.norm = d->norm_type;
-    gb.A = L.G1; gb.lda = d->H;
-    gb.W = w1t; gb.ldw = d->H;
-    gb.epi = EPI_RESID; gb.R = gy; gb.ldr = d->B;
-    gb.C = gx; gb.ldc = d->B;
+  const bool fused1 = fold && tb_fused_n1(d);
+  int nalpha = ew_blocks(da);
+  if (fused1) {
+    // (d+e) gx = n1bwd(G2) . W1 + gy; the operand stage applies the norm-1/PReLU-1
+    //       backward (norm-1 sums folded from dw_bwd's slab), sums the alpha-1
+    //       gradient and stores gh1 = dL/dh1 to G1 on the way (one pass instead of
+    //       norm1_bwd's write + the GEMM's re-read)
+    GemmRows gb = tb_gemmB(d, true);
+    gb.A = L.G2; gb.W = w1t; gb.R = gy; gb.C = gx;
+    gb.aop.stats = st1; gb.aop.alpha = p->alpha1; gb.aop.aux = sv->h1; gb.aop.apart = L.alphaSlab;
+    gb.aop.aout = L.G1;
+    gb.aop.fold = StatFold{L.slabD, L.partsD, cnt, 0.f, 1, nullptr};
     CTN_HIP(launch_gemm_rows(dt, gb, s));
+    nalpha = gemm_ws_grid(gb);
+    // (f) dW1 = gh1^T . x, gh1 = G1 as stored by the kernel above
     GemmCols c1{};
     c1.g = rg; c1.P = d->H; c1.Q = d->B;
     c1.A = L.G1; c1.lda = d->H;
     c1.B = x; c1.ldb = d->B;
     c1.Cpart = L.cpart1; c1.nchunks = L.chunks1;
     CTN_HIP(launch_gemm_cols(dt, c1, s));
+  } else {
+    if (!fold) CTN_HIP(launch_stats_finalize(L.slabD, G, L.partsD, cnt, 1, 0.f, L.sums1, s));
+    // (d) norm1 backward finish + PReLU1 backward -> G1 = dL/dh1
+    DwArgs de = da;
+    de.ga2 = L.G2; de.sm1 = L.sums1; de.gh1_out = L.G1; de.alpha_slab = L.alphaSlab;
+    de.f_sm2 = StatFold{};
+    if (fold) de.f_sm1 = StatFold{L.slabD, L.partsD, cnt, 0.f, 1, nullptr};
+    CTN_HIP(launch_norm1_bwd(dt, de, s));
+    // (e) gx = gh1 . W1 + gy
+    // (f) dW1 = gh1^T . x                          — one dual-GEMM pass when eligible
+    GemmDual duB = tb_dualB(d);
+    duB.A = L.G1; duB.W = w1t; duB.R = gy; duB.C = gx;
+    duB.Bm = x; duB.Dpart = L.cpart1;
+    if (gemm_dual_eligible(dt, duB)) {
+      CTN_HIP(launch_gemm_dual(duB, s));
+    } else {
+      GemmRows gb{};
+      gb.g = rg; gb.Kred = d->H; gb.Nout = d->B; gb.norm = d->norm_type;
+      gb.A = L.G1; gb.lda = d->H;
+      gb.W = w1t; gb.ldw = d->H;
+      gb.epi = EPI_RESID; gb.R = gy; gb.ldr = d->B;
+      gb.C = gx; gb.ldc = d->B;
+      CTN_HIP(launch_gemm_rows(dt, gb, s));
+      GemmCols c1{};
+      c1.g = rg; c1.P = d->H; c1.Q = d->B;
+      c1.A = L.G1; c1.lda = d->H;
+      c1.B = x; c1.ldb = d->B;
+      c1.Cpart = L.cpart1; c1.nchunks = L.chunks1;
+      CTN_HIP(launch_gemm_cols(dt, c1, s));
+    }
   }
   // (g) all parameter-gradient partial sums
   const int dwb = dw_blocks(da), dws = dw_col_stride(da);
@@ -452,7 +502,7 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
   sb.d[5] = SlabDesc{L.colD + H, gr->beta1, dwb, H, dws};
   sb.d[6] = SlabDesc{L.colD + 2 * H, gr->wd, dwb, H * d->P, dws};
   sb.d[7] = SlabDesc{L.colD + (4 + d->P) * H, gr->alpha2, dwb, 1, dws};
-  sb.d[8] = SlabDesc{L.alphaSlab, gr->alpha1, ew_blocks(da), 1, 1};
+  sb.d[8] = SlabDesc{L.alphaSlab, gr->alpha1, nalpha, 1, 1};
   sb.nd = 9;
   CTN_HIP(launch_slab_reduce(sb, L.srtmp, s));
   return CTN_OK;

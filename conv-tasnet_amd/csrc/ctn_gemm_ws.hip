@@ -68,12 +68,15 @@ __global__ __launch_bounds__(64 * WV) void gemm_ws_kernel(GemmRows p) {
   static_assert(NA >= 1 && NA * NT == TM * CPR, "tile/thread mismatch");
   static_assert(Q >= 1, "at least 8 channels per lane");
   // one-tile register prefetch + two accumulator sets only where registers allow
+  constexpr bool N1B = OPK == OP_NORM1_BWD;    // norm-1/PReLU-1 backward on the operand
   constexpr bool SWP = OPK == OP_PLAIN && WV == 8;
   __shared__ __attribute__((aligned(16))) char sA[2][TM * KR * 2];
   __shared__ float sgam[EPI == EPI_NORM_BWD ? NB * 16 * WV : 1];
   // gLN operand statistics, one pair per utterance, finalized here (StatFold)
   constexpr bool FOLDS = NK == NORM_GLN && OPK != OP_PLAIN;
   __shared__ float2 sst[FOLDS ? WS_FOLD_MAX : 1];
+  __shared__ float2 sst1[N1B ? WS_FOLD_MAX : 1];   // N1B: forward norm-1 (mean, rstd); sst holds the sums
+  __shared__ float salpha[N1B ? WV : 1];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
@@ -105,22 +108,30 @@ __global__ __launch_bounds__(64 * WV) void gemm_ws_kernel(GemmRows p) {
         }
       }
     } else {
-      for (int gi = tid; gi < p.g.M; gi += NT) sst[gi] = p.aop.stats[gi];
+      const float2* tab = N1B ? p.aop.sums : p.aop.stats;
+      for (int gi = tid; gi < p.g.M; gi += NT) sst[gi] = tab[gi];
     }
+    if constexpr (N1B)
+      for (int gi = tid; gi < p.g.M; gi += NT) sst1[gi] = p.aop.stats[gi];
     __syncthreads();
   }
 
   // ---- A staging: thread owns k-chunk kc (fixed) of rows rl0 + j*RSTEP
   const int kc = tid % CPR, rl0 = tid / CPR;
   float og[8], ob[8];
-  if constexpr (OPK != OP_PLAIN) {
+  constexpr bool AFF = OPK == OP_NORM || OPK == OP_PRELU_NORM;   // operand op with gamma/beta
+  if constexpr (AFF) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       og[e] = p.aop.gamma[kc * 8 + e];
       ob[e] = p.aop.beta[kc * 8 + e];
     }
   }
-  const float oal = (OPK == OP_PRELU_NORM) ? p.aop.alpha[0] : 0.f;
+  const float oal = (OPK == OP_PRELU_NORM || N1B) ? p.aop.alpha[0] : 0.f;
+  const bf16raw* H1 = reinterpret_cast<const bf16raw*>(p.aop.aux);
+  bf16raw* GH = reinterpret_cast<bf16raw*>(p.aop.aout);
+  v4u rh[N1B ? NA : 1];   // N1B: h1 chunks beside the gradient chunks
+  float calpha = 0.f;     // N1B: this thread's PReLU-1 alpha gradient over its valid rows
   // Loads are issued one tile ahead together with the statistics they need, so
   // that no wait inside an iteration has to drain the next tile's prefetch
   // (vmcnt retires loads in issue order).
@@ -132,20 +143,46 @@ __global__ __launch_bounds__(64 * WV) void gemm_ws_kernel(GemmRows p) {
       const int r = t * TM + rl0 + j * RSTEP;
       if constexpr (CTN_WS_EXP & 2) ra[j] = v4u{(uint32_t)r, 0u, 0u, 0u};
       else ra[j] = ldg16(A + (size_t)r * p.lda + kc * 8);
+      if constexpr (N1B) rh[j] = ldg16(H1 + (size_t)r * p.lda + kc * 8);
       if constexpr (OPK != OP_PLAIN && !FOLDS) ast[j] = p.aop.stats[stat_index<NK>(r, Kp)];
     }
   };
   // ra -> LDS image of tile t (fragment (mb, kb) at (mb*KB + kb) KiB).  Rows of padded
   // frames are staged as zeros, so every output row of a padded frame is exactly 0
   // (+ the residual's zero row) and contributes nothing to any statistic.
-  auto stage = [&](auto le1, int t, char* buf) __attribute__((always_inline)) {
+  // tu may run past the range: such tiles are clamped to the last one (staged again,
+  // never stored, and not counted in the alpha gradient).
+  auto stage = [&](auto le1, int tu, char* buf) __attribute__((always_inline)) {
     constexpr bool LE1 = decltype(le1)::value;
+    const int t = tu < t1 ? tu : t1 - 1;
     const int tk = (t * TM) % Kp;   // frame index of the tile's first row (wave-uniform)
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
       v4u v = ra[j];
       const int r = rl0 + j * RSTEP;
-      if constexpr (OPK != OP_PLAIN) {
+      if constexpr (N1B) {
+        // same arithmetic as norm1_bwd_kernel (ctn_tcn.hip), element by element
+        const int m = (t * TM) / Kp;
+        const float2 sm = sst[m], st = sst1[m];
+        float g[8], h[8];
+        unpack_bf16x8(v, g);
+        unpack_bf16x8(rh[j], h);
+        float ca = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float o[2];
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const float hv = h[2 * e + u];
+            const float ah = (prelu(hv, oal) - st.x) * st.y;
+            const float ga = st.y * (g[2 * e + u] - sm.x - ah * sm.y);
+            o[u] = ga * prelu_dx(hv, oal);
+            ca += ga * prelu_da(hv);
+          }
+          v[e] = pk_bf16(o[0], o[1]);
+        }
+        calpha += (tu < t1 && tk + r < Kv) ? ca : 0.f;
+      } else if constexpr (OPK != OP_PLAIN) {
         const float2 st = FOLDS ? sst[(t * TM) / Kp] : ast[j];
         float f[8];
         unpack_bf16x8(v, f);
@@ -160,6 +197,8 @@ __global__ __launch_bounds__(64 * WV) void gemm_ws_kernel(GemmRows p) {
       }
       const v4u z = v4u{0u, 0u, 0u, 0u};
       v = tk + r < Kv ? v : z;   // tiles never straddle utterances (Kp % TM == 0)
+      if constexpr (N1B)         // dL/dh1 for the weight-gradient kernel (padded rows 0)
+        if (tu < t1) stg16(GH + (size_t)(t * TM + r) * p.lda + kc * 8, v);
       stg16(buf + (r >> 4) * KB * 1024 + ws_slot(r & 15, kc & 3, kc >> 2), v);
     }
   };
@@ -310,7 +349,7 @@ __global__ __launch_bounds__(64 * WV) void gemm_ws_kernel(GemmRows p) {
   for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) ready(wf[nb][kb]);
-  if constexpr (OPK != OP_PLAIN) {
+  if constexpr (AFF) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) { ready(og[e]); ready(ob[e]); }
   }
@@ -339,7 +378,7 @@ __global__ __launch_bounds__(64 * WV) void gemm_ws_kernel(GemmRows p) {
         __builtin_amdgcn_sched_barrier(0);
         epilogue(le1, t, acc);
         load_r(clampt(t + 1));
-        stage(le1, clampt(t + 1), sA[(t + 1) & 1]);
+        stage(le1, t + 1, sA[(t + 1) & 1]);
         load_a(clampt(t + 2));
       }
     } else {
@@ -350,7 +389,7 @@ __global__ __launch_bounds__(64 * WV) void gemm_ws_kernel(GemmRows p) {
       lds_barrier();
       mfma_tile(sA[t0 & 1], accP);
       load_r(t0);
-      stage(le1, clampt(t0 + 1), sA[(t0 + 1) & 1]);
+      stage(le1, t0 + 1, sA[(t0 + 1) & 1]);
       load_a(clampt(t0 + 2));
       // unrolled by two so the two accumulator sets swap roles without copies
       auto step = [&](int t, f32x4_t (&cur)[MB][NB], f32x4_t (&prev)[MB][NB]) __attribute__((always_inline)) {
@@ -358,7 +397,7 @@ __global__ __launch_bounds__(64 * WV) void gemm_ws_kernel(GemmRows p) {
         mfma_tile(sA[t & 1], cur);
         epilogue(le1, t - 1, prev);
         load_r(t);
-        stage(le1, clampt(t + 1), sA[(t + 1) & 1]);
+        stage(le1, t + 1, sA[(t + 1) & 1]);
         load_a(clampt(t + 2));
       };
       int t = t0 + 1;
@@ -374,14 +413,24 @@ __global__ __launch_bounds__(64 * WV) void gemm_ws_kernel(GemmRows p) {
       }
     }
   };
-  const float al_any = OPK == OP_PRELU_NORM ? oal : eal;
-  if constexpr (OPK == OP_PRELU_NORM || HAS_STATS) {
+  const float al_any = (OPK == OP_PRELU_NORM || N1B) ? oal : eal;
+  if constexpr (OPK == OP_PRELU_NORM || N1B || HAS_STATS) {
     if (al_any <= 1.f) run(std::true_type{});
     else run(std::false_type{});
   } else {
     run(std::true_type{});
   }
   if constexpr (HAS_STATS && NK == NORM_GLN) flush_run();
+  if constexpr (N1B) {   // fixed-order workgroup sum of the alpha-gradient partials
+    const float w = wave_sum_dpp(calpha);
+    if (lane == 0) salpha[wid] = w;
+    __syncthreads();
+    if (tid == 0) {
+      double a = 0.0;
+      for (int i = 0; i < WV; ++i) a += (double)salpha[i];
+      p.aop.apart[blockIdx.x] = (float)a;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -406,7 +455,8 @@ static bool ws_shape(int Nout, int Kred, int* nb, int* kb) {
 
 static bool ws_pair(int opk, int epi) {   // (operand op, epilogue) pairs used on the path
   return (opk == OP_PLAIN && (epi == EPI_PRELU_STATS || epi == EPI_NORM_BWD || epi == EPI_RESID || epi == EPI_STORE)) ||
-         (opk == OP_PRELU_NORM && epi == EPI_RESID) || (opk == OP_NORM && epi == EPI_STORE);
+         (opk == OP_PRELU_NORM && epi == EPI_RESID) || (opk == OP_NORM && epi == EPI_STORE) ||
+         (opk == OP_NORM1_BWD && epi == EPI_RESID);
 }
 
 bool gemm_ws_eligible(DType dt, const GemmRows& p) {
@@ -415,6 +465,9 @@ bool gemm_ws_eligible(DType dt, const GemmRows& p) {
   if (p.g.Kp % WS_TM || p.lda % 8 || p.ldw % 8 || p.ldc % 8) return false;
   if ((p.epi == EPI_RESID || p.epi == EPI_NORM_BWD) && p.ldr % 8) return false;
   if (p.aop.kind != OP_PLAIN && p.aop.norm == NORM_GLN && p.g.M > WS_FOLD_MAX) return false;
+  if (p.aop.kind == OP_NORM1_BWD && (p.aop.norm != NORM_GLN || !p.aop.aux || !p.aop.aout || !p.aop.apart ||
+                                     !p.aop.stats || (!p.aop.fold.slab && !p.aop.sums)))
+    return false;
   return true;
 }
 
@@ -482,6 +535,10 @@ static int ws_tile_rows(const GemmRows& p) { return ws_wide(p) ? 32 : WS_TM; }
 template <int NK>
 static hipError_t ws_launch_nk(const GemmRows& p, hipStream_t s) {
   if (p.aop.kind == OP_PRELU_NORM) return ws_launch_shape<OP_PRELU_NORM, NK, EPI_RESID>(p, s);
+  if (p.aop.kind == OP_NORM1_BWD) {
+    if constexpr (NK == NORM_GLN) return ws_launch_shape<OP_NORM1_BWD, NK, EPI_RESID>(p, s);
+    return hipErrorInvalidValue;
+  }
   if (p.aop.kind == OP_NORM) return ws_launch_shape<OP_NORM, NK, EPI_STORE>(p, s);
   switch (p.epi) {
     case EPI_PRELU_STATS: return ws_launch_shape<OP_PLAIN, NK, EPI_PRELU_STATS>(p, s);

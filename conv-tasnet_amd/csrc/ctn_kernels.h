@@ -10,7 +10,12 @@
 namespace ctn {
 
 enum DType { F32 = 0, BF16 = 1 };
-enum RowOpKind { OP_PLAIN = 0, OP_NORM = 1, OP_PRELU_NORM = 2 };
+// OP_NORM1_BWD (bf16, gLN; WS kernel, the first 1x1's data gradient): the operand
+// is g = dL/d(hat a1) and becomes dL/dh1 = PReLU'(h1) * rstd * (g - mean g - hat a1 *
+// mean(g hat a1)) on the way into LDS (conv_tasnet.py:217-219 backward), with
+// h1 = `aux`, (mean, rstd) = `stats`, the two means = `sums` or `fold`; dL/dh1 is
+// also stored (`aout`) for the weight-gradient kernel.
+enum RowOpKind { OP_PLAIN = 0, OP_NORM = 1, OP_PRELU_NORM = 2, OP_NORM1_BWD = 3 };
 enum EpiKind { EPI_STORE = 0, EPI_PRELU_STATS = 1, EPI_RESID = 2, EPI_NORM_BWD = 3 };
 
 // element-wise transform applied to an operand row while it is staged into LDS
@@ -21,7 +26,12 @@ struct RowOp {
   const float* gamma = nullptr;
   const float* beta = nullptr;
   const float* alpha = nullptr;    // PReLU alpha (device pointer, 1 element)
-  StatFold fold;                   // gLN: finalize `stats` in the consumer (WS kernel only)
+  StatFold fold;                   // gLN: finalize `stats` (OP_NORM1_BWD: `sums`) in the consumer (WS kernel only)
+  // OP_NORM1_BWD only
+  const void* aux = nullptr;       // h1, same layout as the operand
+  const float2* sums = nullptr;    // (mean g, mean g*hat a1) per utterance, when not folded
+  void* aout = nullptr;            // WS kernel: the transformed operand dL/dh1 is stored here too
+  float* apart = nullptr;          // WS kernel: one PReLU-alpha gradient partial per workgroup
 };
 
 // Geometry of a frame-row tensor set: rows = M * Kp, valid frames K per utterance.
