@@ -39,7 +39,7 @@ def _norm_code(norm_type):
         return L.NORM_GLN
     if norm_type == "cLN":
         return L.NORM_CLN
-    raise L.CtnLibraryError(f"norm_type {norm_type!r} (BatchNorm) is not implemented by the HIP path")
+    return L.NORM_BN      # chose_norm's fallback branch: nn.BatchNorm1d (conv_tasnet.py:302-303)
 
 
 def _mask_code(mask_nonlinear):
@@ -222,16 +222,25 @@ class TemporalBlock(nn.Module):
         if stride != 1:
             raise ValueError("TemporalBlock: only stride 1 is used by the reference (conv_tasnet.py:177)")
 
+    def _norms(self):
+        ds = self.net[3].net
+        return self.net[2], ds[3 if self._geo[4] else 2]
+
     def _params(self):
         ds = self.net[3].net
         off = 1 if self._geo[4] else 0
-        n1, n2 = self.net[2], ds[2 + off]
-        return (self.net[0].weight, self.net[1].weight, n1.gamma, n1.beta, ds[0].weight,
-                ds[1 + off].weight, n2.gamma, n2.beta, ds[3 + off].weight)
+        n1, n2 = self._norms()
+        if isinstance(n1, nn.BatchNorm1d):
+            g1, b1, g2, b2 = n1.weight, n1.bias, n2.weight, n2.bias
+        else:
+            g1, b1, g2, b2 = n1.gamma, n1.beta, n2.gamma, n2.beta
+        return (self.net[0].weight, self.net[1].weight, g1, b1, ds[0].weight,
+                ds[1 + off].weight, g2, b2, ds[3 + off].weight)
 
     def _forward_rows(self, x_rows, fr, norm, pack=None):
         B, H, P, dil, causal, _ = self._geo
-        return ops.TBlockFn.apply(x_rows, fr, (B, H, P, dil, causal, norm), pack, *self._params())
+        bn = ops.bn_state(*self._norms()) if norm == L.NORM_BN else None
+        return ops.TBlockFn.apply(x_rows, fr, (B, H, P, dil, causal, norm), pack, bn, *self._params())
 
     def forward(self, x):
         """x [M, B, K] -> [M, B, K]."""

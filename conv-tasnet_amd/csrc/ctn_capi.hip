@@ -128,8 +128,8 @@ static int tb_check(const ctn_tblock_desc* d) {
   if (d->P < 1 || d->P > 8) return fail(CTN_ERR_UNSUPPORTED, "P=%d outside 1..8", d->P);
   if (!d->causal && d->P % 2 == 0)
     return fail(CTN_ERR_ARG, "non-causal padding (P-1)*d//2 needs odd P (conv_tasnet.py:236)");
-  if (d->norm_type != CTN_NORM_GLN && d->norm_type != CTN_NORM_CLN)
-    return fail(CTN_ERR_UNSUPPORTED, "norm_type %d (BN) not implemented on the HIP path", d->norm_type);
+  if (d->norm_type != CTN_NORM_GLN && d->norm_type != CTN_NORM_CLN && d->norm_type != CTN_NORM_BN)
+    return fail(CTN_ERR_ARG, "norm_type %d", d->norm_type);
   {
     const int cg = d->H / 8;
     if (cg > 64 || (cg & (cg - 1))) return fail(CTN_ERR_UNSUPPORTED, "H=%d: need H/8 a power of two <= 64", d->H);
@@ -139,7 +139,10 @@ static int tb_check(const ctn_tblock_desc* d) {
   return CTN_OK;
 }
 
-static int tb_groups(const ctn_tblock_desc* d) { return d->norm_type == CTN_NORM_GLN ? d->M : d->M * d->Kp; }
+static int tb_groups(const ctn_tblock_desc* d) {
+  if (d->norm_type == CTN_NORM_BN) return d->H;   // per-channel statistics
+  return d->norm_type == CTN_NORM_GLN ? d->M : d->M * d->Kp;
+}
 
 extern "C" int ctn_tblock_stats_floats(const ctn_tblock_desc* d) { return 4 * tb_groups(d); }
 
@@ -286,8 +289,259 @@ TbLayout tb_layout(const ctn_tblock_desc* d, int backward, void* ws) {
 
 }  // namespace
 
+// ===========================================================================
+// TemporalBlock with BatchNorm1d norms (norm_type "BN", conv_tasnet.py:302-303)
+// ===========================================================================
+// The block's kernels run in identity gLN mode (per-utterance stats (0, 1),
+// gamma' = gamma*rstd, beta' = beta - gamma*mean*rstd per channel, ctn_bn.hip);
+// BN's per-channel statistics and the per-channel mean subtractions of its
+// backward run in the column kernels of ctn_bn.hip.
+namespace {
+struct BnLayout {
+  void *w1s, *w2s, *w1t, *w2t, *G1, *G2;
+  double2 *part, *slab2, *slabD;
+  float2 *ident, *zero, *sums1, *sums2;
+  float *ge1, *be1, *ge2, *be2, *colD, *alphaSlab, *cpart1, *cpart2, *srtmp;
+  int chunks1, chunks2;
+  size_t bytes;
+};
+DwArgs bn_dw(const ctn_tblock_desc* d, bool bwd) {
+  DwArgs da{};
+  da.g = Rows{d->M, d->K, d->Kp};
+  da.H = d->H; da.P = d->P; da.dil = d->dilation; da.pad = tb_pad(d); da.norm = NORM_GLN;
+  da.seg = dw_seg(da, bwd);
+  return da;
+}
+BnLayout bn_layout(const ctn_tblock_desc* d, int backward, void* ws) {
+  BnLayout L{};
+  Carver c(ws);
+  const Rows rg{d->M, d->K, d->Kp};
+  const long rows = rg.rows();
+  const size_t es = esize(d->dtype);
+  const int H = d->H, B = d->B, M = d->M, nb = bn_blocks(rg);
+  L.part = c.take<double2>((size_t)nb * H * sizeof(double2));
+  L.ident = c.take<float2>((size_t)M * sizeof(float2));
+  L.zero = c.take<float2>((size_t)M * sizeof(float2));
+  L.ge1 = c.take<float>((size_t)H * sizeof(float));
+  L.be1 = c.take<float>((size_t)H * sizeof(float));
+  L.ge2 = c.take<float>((size_t)H * sizeof(float));
+  L.be2 = c.take<float>((size_t)H * sizeof(float));
+  if (!backward) {
+    if (d->dtype == CTN_DTYPE_BF16) {
+      L.w1s = c.take<void>((size_t)H * B * es);
+      L.w2s = c.take<void>((size_t)H * B * es);
+    }
+    const DwArgs da = bn_dw(d, false);
+    L.slab2 = c.take<double2>((size_t)M * dw_parts_per_group(da) * sizeof(double2));
+  } else {
+    L.w1t = c.take<void>((size_t)H * B * es);
+    L.w2t = c.take<void>((size_t)H * B * es);
+    L.G1 = c.take<void>((size_t)rows * H * es);
+    L.G2 = c.take<void>((size_t)rows * H * es);
+    L.sums1 = c.take<float2>((size_t)H * sizeof(float2));
+    L.sums2 = c.take<float2>((size_t)H * sizeof(float2));
+    const DwArgs da = bn_dw(d, true);
+    L.slabD = c.take<double2>((size_t)M * dw_parts_per_group(da) * sizeof(double2));
+    L.colD = c.take<float>((size_t)dw_blocks(da) * dw_col_stride(da) * sizeof(float));
+    L.alphaSlab = c.take<float>((size_t)nb * sizeof(float));
+    GemmCols gc{};
+    gc.g = rg; gc.P = B; gc.Q = H;
+    L.chunks2 = gemm_cols_default_chunks(gc);
+    L.cpart2 = c.take<float>((size_t)L.chunks2 * B * H * sizeof(float));
+    gc.P = H; gc.Q = B;
+    L.chunks1 = gemm_cols_default_chunks(gc);
+    L.cpart1 = c.take<float>((size_t)L.chunks1 * B * H * sizeof(float));
+    const long HB = (long)H * B, dwb = dw_blocks(da);
+    const size_t ntmp = sr_tmp(L.chunks2, HB) + sr_tmp(L.chunks1, HB) + 2 * sr_tmp(dwb, H) +
+                        sr_tmp(dwb, (long)H * d->P) + sr_tmp(dwb, 1) + sr_tmp(nb, 1);
+    L.srtmp = c.take<float>(ntmp * sizeof(float));
+  }
+  L.bytes = c.off + 256;
+  return L;
+}
+
+// forward statistics of PReLU(a) -> stats, gamma', beta', running statistics
+int bn_forward_stats(DType dt, const ctn_tblock_desc* d, const BnLayout& L, const void* a, const float* alpha,
+                     const float* gamma, const float* beta, float* rmean, float* rvar, int training, float mom,
+                     float eps, float2* stats, float* ge, float* be, hipStream_t s) {
+  const Rows rg{d->M, d->K, d->Kp};
+  const bool batch = training || !rmean;
+  if (!batch && !rvar) return fail(CTN_ERR_ARG, "BN eval mode needs running_var");
+  if (batch) {
+    BnArgs ba{};
+    ba.g = rg; ba.H = d->H; ba.a = a; ba.alpha = alpha; ba.part = L.part;
+    CTN_HIP(launch_bn_partials(dt, ba, 0, s));
+  }
+  BnFinal bf{};
+  bf.H = d->H; bf.M = d->M; bf.nparts = bn_blocks(rg); bf.count = (long)d->M * d->K; bf.part = L.part;
+  bf.training = batch; bf.momentum = mom; bf.eps = eps;
+  bf.run_mean = training ? rmean : (batch ? nullptr : rmean);
+  bf.run_var = training ? rvar : (batch ? nullptr : rvar);
+  bf.gamma = gamma; bf.beta = beta; bf.stats = stats; bf.gamma_eff = ge; bf.beta_eff = be;
+  bf.ident = L.ident; bf.zero = L.zero;
+  CTN_HIP(launch_bn_finalize(bf, 0, s));
+  return CTN_OK;
+}
+}  // namespace
+
+static int tb_forward_bn(const ctn_tblock_desc* d, const ctn_tblock_params* p, const void* x, void* y,
+                         const ctn_tblock_saved* sv, void* ws, size_t ws_bytes, hipStream_t s) {
+  const BnLayout L = bn_layout(d, 0, ws);
+  if (!ws || ws_bytes < L.bytes) return fail(CTN_ERR_WORKSPACE, "workspace %zu < %zu", ws_bytes, L.bytes);
+  const DType dt = tb_dt(d);
+  const Rows rg{d->M, d->K, d->Kp};
+  float2* st1 = reinterpret_cast<float2*>(sv->stats);
+  float2* st2 = st1 + d->H;
+  const void* w1 = p->w1;
+  const void* w2 = p->w2;
+  if (dt == BF16 && p->w1_bf16 && p->w2_bf16) {
+    w1 = p->w1_bf16;
+    w2 = p->w2_bf16;
+  } else if (dt == BF16) {
+    PrepBatch pb{};
+    pb.d[0] = PrepDesc{p->w1, d->H, d->B, L.w1s, nullptr};
+    pb.d[1] = PrepDesc{p->w2, d->B, d->H, L.w2s, nullptr};
+    pb.nd = 2;
+    CTN_HIP(launch_prep_weights(dt, pb, s));
+    w1 = L.w1s;
+    w2 = L.w2s;
+  }
+  // 1x1 conv B->H (pre-PReLU h1)
+  GemmRows g1{};
+  g1.g = rg; g1.Kred = d->B; g1.Nout = d->H; g1.norm = NORM_GLN;
+  g1.A = x; g1.lda = d->B; g1.W = w1; g1.ldw = d->B; g1.epi = EPI_STORE; g1.C = sv->h1; g1.ldc = d->H;
+  CTN_HIP(launch_gemm_rows(dt, g1, s));
+  // BN-1 statistics of PReLU(h1)
+  int rc = bn_forward_stats(dt, d, L, sv->h1, p->alpha1, p->gamma1, p->beta1, p->bn_mean1, p->bn_var1,
+                            p->bn_training, p->bn_momentum1, p->bn_eps1, st1, L.ge1, L.be1, s);
+  if (rc) return rc;
+  // BN-1 apply (identity gLN) + dilated depthwise conv
+  DwArgs da = bn_dw(d, false);
+  da.h1 = sv->h1; da.st1 = L.ident;
+  da.alpha1 = p->alpha1; da.gamma1 = L.ge1; da.beta1 = L.be1; da.alpha2 = p->alpha2;
+  da.wd = p->wd; da.d_out = sv->d; da.slab2 = L.slab2;
+  CTN_HIP(launch_dw_fwd(dt, da, s));
+  // BN-2 statistics of PReLU(d)
+  rc = bn_forward_stats(dt, d, L, sv->d, p->alpha2, p->gamma2, p->beta2, p->bn_mean2, p->bn_var2,
+                        p->bn_training, p->bn_momentum2, p->bn_eps2, st2, L.ge2, L.be2, s);
+  if (rc) return rc;
+  // BN-2 apply (identity gLN, with PReLU) on the operand, 1x1 conv H->B, residual
+  GemmRows g2{};
+  g2.g = rg; g2.Kred = d->H; g2.Nout = d->B; g2.norm = NORM_GLN;
+  g2.A = sv->d; g2.lda = d->H;
+  g2.aop.kind = OP_PRELU_NORM; g2.aop.norm = NORM_GLN; g2.aop.stats = L.ident;
+  g2.aop.gamma = L.ge2; g2.aop.beta = L.be2; g2.aop.alpha = p->alpha2;
+  g2.W = w2; g2.ldw = d->H;
+  g2.epi = EPI_RESID; g2.R = x; g2.ldr = d->B;
+  g2.C = y; g2.ldc = d->B;
+  CTN_HIP(launch_gemm_rows(dt, g2, s));
+  return CTN_OK;
+}
+
+static int tb_backward_bn(const ctn_tblock_desc* d, const ctn_tblock_params* p, const void* x,
+                          const ctn_tblock_saved* sv, const void* gy, void* gx, const ctn_tblock_grads* gr, void* ws,
+                          size_t ws_bytes, hipStream_t s) {
+  const BnLayout L = bn_layout(d, 1, ws);
+  if (!ws || ws_bytes < L.bytes) return fail(CTN_ERR_WORKSPACE, "workspace %zu < %zu", ws_bytes, L.bytes);
+  const DType dt = tb_dt(d);
+  const Rows rg{d->M, d->K, d->Kp};
+  const int H = d->H, nb = bn_blocks(rg);
+  const float2* st1 = reinterpret_cast<const float2*>(sv->stats);
+  const float2* st2 = st1 + H;
+  const int train1 = p->bn_training || !p->bn_mean1, train2 = p->bn_training || !p->bn_mean2;
+
+  const void* w1t = L.w1t;
+  const void* w2t = L.w2t;
+  if (dt == BF16 && p->w1t_bf16 && p->w2t_bf16) {
+    w1t = p->w1t_bf16;
+    w2t = p->w2t_bf16;
+  } else {
+    PrepBatch pb{};
+    pb.d[0] = PrepDesc{p->w2, d->B, H, nullptr, L.w2t};
+    pb.d[1] = PrepDesc{p->w1, H, d->B, nullptr, L.w1t};
+    pb.nd = 2;
+    CTN_HIP(launch_prep_weights(dt, pb, s));
+  }
+  // gamma' / beta' from the saved statistics; identity and zero tables
+  {
+    BnFinal pf{};
+    pf.H = H; pf.M = d->M; pf.gamma = p->gamma1; pf.beta = p->beta1; pf.stats = const_cast<float2*>(st1);
+    pf.gamma_eff = L.ge1; pf.beta_eff = L.be1; pf.ident = L.ident; pf.zero = L.zero;
+    CTN_HIP(launch_bn_finalize(pf, 2, s));
+    pf.gamma = p->gamma2; pf.beta = p->beta2; pf.stats = const_cast<float2*>(st2);
+    pf.gamma_eff = L.ge2; pf.beta_eff = L.be2; pf.ident = nullptr; pf.zero = nullptr;
+    CTN_HIP(launch_bn_finalize(pf, 2, s));
+  }
+  // (a) G1 = dL/dn2 = gy . W2
+  GemmRows ga{};
+  ga.g = rg; ga.Kred = d->B; ga.Nout = H; ga.norm = NORM_GLN;
+  ga.A = gy; ga.lda = d->B; ga.W = w2t; ga.ldw = d->B; ga.epi = EPI_STORE; ga.C = L.G1; ga.ldc = H;
+  CTN_HIP(launch_gemm_rows(dt, ga, s));
+  // (b) dW2 partials = gy^T . BN2(PReLU(d))
+  GemmCols c2{};
+  c2.g = rg; c2.P = d->B; c2.Q = H;
+  c2.A = gy; c2.lda = d->B;
+  c2.B = sv->d; c2.ldb = H;
+  c2.bop.kind = OP_PRELU_NORM; c2.bop.norm = NORM_GLN; c2.bop.stats = L.ident;
+  c2.bop.gamma = L.ge2; c2.bop.beta = L.be2; c2.bop.alpha = p->alpha2;
+  c2.Cpart = L.cpart2; c2.nchunks = L.chunks2;
+  CTN_HIP(launch_gemm_cols(dt, c2, s));
+  // (c) BN-2 backward sums (= beta2 / gamma2 gradients) and (d) G1 -= per-channel means
+  BnArgs ba{};
+  ba.g = rg; ba.H = H; ba.part = L.part;
+  ba.a = sv->d; ba.gin = L.G1; ba.gout = L.G1; ba.alpha = p->alpha2; ba.stats = st2; ba.sums = L.sums2;
+  CTN_HIP(launch_bn_partials(dt, ba, 1, s));
+  BnFinal bf{};
+  bf.H = H; bf.M = d->M; bf.nparts = nb; bf.count = (long)d->M * d->K; bf.part = L.part;
+  bf.training = train2; bf.sums = L.sums2; bf.dgamma = gr->gamma2; bf.dbeta = gr->beta2;
+  CTN_HIP(launch_bn_finalize(bf, 1, s));
+  CTN_HIP(launch_bn_apply(dt, ba, false, s));
+  // (e) depthwise backward in identity mode -> G2 = dL/dn1 * gamma1' ; wd, alpha2 and
+  //     (gamma1', beta1') column partials
+  DwArgs da = bn_dw(d, true);
+  da.h1 = sv->h1; da.d = sv->d; da.st1 = L.ident; da.st2 = L.ident;
+  da.alpha1 = p->alpha1; da.gamma1 = L.ge1; da.beta1 = L.be1; da.alpha2 = p->alpha2; da.gamma2 = L.ge2;
+  da.wd = p->wd;
+  da.ga2 = L.G1; da.sm2 = L.zero; da.ga1_out = L.G2; da.slab1 = L.slabD; da.col_slab = L.colD;
+  CTN_HIP(launch_dw_bwd(dt, da, s));
+  // (f) BN-1 backward sums over (G2, h1), (g) G1 = (G2 - means) * PReLU'(h1), alpha-1 partials
+  ba.a = sv->h1; ba.gin = L.G2; ba.gout = L.G1; ba.alpha = p->alpha1; ba.stats = st1; ba.sums = L.sums1;
+  ba.apart = L.alphaSlab;
+  CTN_HIP(launch_bn_partials(dt, ba, 1, s));
+  bf.training = train1; bf.sums = L.sums1; bf.dgamma = nullptr; bf.dbeta = nullptr;
+  CTN_HIP(launch_bn_finalize(bf, 1, s));
+  CTN_HIP(launch_bn_apply(dt, ba, true, s));
+  // (h) gx = G1 . W1 + gy ; dW1 partials = G1^T . x
+  GemmRows gb{};
+  gb.g = rg; gb.Kred = H; gb.Nout = d->B; gb.norm = NORM_GLN;
+  gb.A = L.G1; gb.lda = H; gb.W = w1t; gb.ldw = H;
+  gb.epi = EPI_RESID; gb.R = gy; gb.ldr = d->B; gb.C = gx; gb.ldc = d->B;
+  CTN_HIP(launch_gemm_rows(dt, gb, s));
+  GemmCols c1{};
+  c1.g = rg; c1.P = H; c1.Q = d->B;
+  c1.A = L.G1; c1.lda = H; c1.B = x; c1.ldb = d->B;
+  c1.Cpart = L.cpart1; c1.nchunks = L.chunks1;
+  CTN_HIP(launch_gemm_cols(dt, c1, s));
+  // (i) parameter-gradient partial sums, (j) gamma1 from the identity-mode (gamma1', beta1')
+  const int dwb = dw_blocks(da), dws = dw_col_stride(da);
+  const int HB = H * d->B;
+  SlabBatch sb{};
+  sb.d[0] = SlabDesc{L.cpart2, gr->w2, L.chunks2, HB, HB};
+  sb.d[1] = SlabDesc{L.cpart1, gr->w1, L.chunks1, HB, HB};
+  sb.d[2] = SlabDesc{L.colD, gr->gamma1, dwb, H, dws};
+  sb.d[3] = SlabDesc{L.colD + H, gr->beta1, dwb, H, dws};
+  sb.d[4] = SlabDesc{L.colD + 2 * H, gr->wd, dwb, H * d->P, dws};
+  sb.d[5] = SlabDesc{L.colD + (4 + d->P) * H, gr->alpha2, dwb, 1, dws};
+  sb.d[6] = SlabDesc{L.alphaSlab, gr->alpha1, nb, 1, 1};
+  sb.nd = 7;
+  CTN_HIP(launch_slab_reduce(sb, L.srtmp, s));
+  CTN_HIP(launch_bn_gamma_fix(gr->gamma1, gr->beta1, st1, H, s));
+  return CTN_OK;
+}
+
 extern "C" size_t ctn_tblock_workspace_bytes(const ctn_tblock_desc* d, int backward) {
   if (tb_check(d) != CTN_OK) return 0;
+  if (d->norm_type == CTN_NORM_BN) return bn_layout(d, backward, nullptr).bytes;
   return tb_layout(d, backward, nullptr).bytes;
 }
 
@@ -296,6 +550,7 @@ extern "C" int ctn_tblock_forward(const ctn_tblock_desc* d, const ctn_tblock_par
   int rc = tb_check(d);
   if (rc) return rc;
   if (!p || !x || !y || !sv || !sv->h1 || !sv->d || !sv->stats) return fail(CTN_ERR_ARG, "null pointer");
+  if (d->norm_type == CTN_NORM_BN) return tb_forward_bn(d, p, x, y, sv, ws, ws_bytes, (hipStream_t)stream);
   const TbLayout L = tb_layout(d, 0, ws);
   if (!ws || ws_bytes < L.bytes) return fail(CTN_ERR_WORKSPACE, "workspace %zu < %zu", ws_bytes, L.bytes);
   hipStream_t s = (hipStream_t)stream;
@@ -367,6 +622,7 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
   int rc = tb_check(d);
   if (rc) return rc;
   if (!p || !x || !sv || !gy || !gx || !gr) return fail(CTN_ERR_ARG, "null pointer");
+  if (d->norm_type == CTN_NORM_BN) return tb_backward_bn(d, p, x, sv, gy, gx, gr, ws, ws_bytes, (hipStream_t)stream);
   const TbLayout L = tb_layout(d, 1, ws);
   if (!ws || ws_bytes < L.bytes) return fail(CTN_ERR_WORKSPACE, "workspace %zu < %zu", ws_bytes, L.bytes);
   hipStream_t s = (hipStream_t)stream;

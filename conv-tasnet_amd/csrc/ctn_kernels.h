@@ -184,6 +184,39 @@ hipError_t launch_dw_fwd(DType dt, const DwArgs& a, hipStream_t s);
 hipError_t launch_dw_bwd(DType dt, const DwArgs& a, hipStream_t s);
 hipError_t launch_norm1_bwd(DType dt, const DwArgs& a, hipStream_t s);
 
+// ---- BatchNorm1d column statistics (ctn_bn.hip) -----------------------------
+struct BnArgs {
+  Rows g;
+  int H;
+  const void* a;          // pre-PReLU activation [rows][H] (h1 or d)
+  const void* gin;        // gradient [rows][H]
+  void* gout;             // bn_apply output (may equal gin)
+  const float* alpha;     // PReLU alpha (1 element)
+  const float2* stats;    // (mean, rstd) per channel
+  const float2* sums;     // (mean g, mean g*xhat) per channel (bn_apply)
+  double2* part;          // [bn_blocks][H] partials (bn_partials)
+  float* apart;           // [bn_blocks] alpha-gradient partials (bn_apply with PReLU)
+};
+struct BnFinal {
+  int H, M, nparts;
+  long count;             // valid frame rows M*K
+  const double2* part;
+  int training;
+  float momentum, eps;
+  float* run_mean; float* run_var;            // may be null (no running statistics)
+  const float* gamma; const float* beta;
+  float2* stats;                              // mode 0 out / mode 2 in
+  float* gamma_eff; float* beta_eff;          // modes 0, 2
+  float2* sums;                               // mode 1
+  float* dgamma; float* dbeta;                // mode 1, optional
+  float2* ident; float2* zero;                // per-utterance (0,1) / (0,0) tables, optional
+};
+int bn_blocks(const Rows& g);
+hipError_t launch_bn_partials(DType dt, const BnArgs& p, int mode, hipStream_t s);
+hipError_t launch_bn_finalize(const BnFinal& p, int mode, hipStream_t s);
+hipError_t launch_bn_apply(DType dt, const BnArgs& p, bool prelu_bwd, hipStream_t s);
+hipError_t launch_bn_gamma_fix(float* dgamma, const float* dbeta, const float2* stats, int H, hipStream_t s);
+
 // ---------------------------------------------------------------------------
 // parameter update (ctn_optim.hip); layouts identical to ctn_opt_segment /
 // ctn_opt_chunk of include/ctn.h

@@ -14,10 +14,10 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CTN_HIP_LIB", os.path.join(_HERE, "libctn_hip.so"))
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 DTYPE_F32, DTYPE_BF16 = 0, 1
-NORM_GLN, NORM_CLN = 0, 1
+NORM_GLN, NORM_CLN, NORM_BN = 0, 1, 2
 MASK_RELU, MASK_SOFTMAX = 0, 1
 ROW_TILE = 128
 
@@ -40,7 +40,10 @@ _TB_PARAM_NAMES = ("w1", "alpha1", "gamma1", "beta1", "wd", "alpha2", "gamma2", 
 
 
 class TBlockParams(ctypes.Structure):
-    _fields_ = [(n, c_void_p) for n in _TB_PARAM_NAMES + ("w1_bf16", "w2_bf16", "w1t_bf16", "w2t_bf16")]
+    _fields_ = ([(n, c_void_p) for n in _TB_PARAM_NAMES + ("w1_bf16", "w2_bf16", "w1t_bf16", "w2t_bf16",
+                                                           "bn_mean1", "bn_var1", "bn_mean2", "bn_var2")] +
+                [("bn_training", c_int32), ("bn_momentum1", ctypes.c_float), ("bn_momentum2", ctypes.c_float),
+                 ("bn_eps1", ctypes.c_float), ("bn_eps2", ctypes.c_float)])
 
 
 class WeightPack(ctypes.Structure):

@@ -79,10 +79,39 @@ class WeightPacks:
         return self.ptrs
 
 
+_NO_BN = (None, None, None, None, 0, 0.0, 0.0, 0.0, 0.0)
+
+
+def bn_state(bn1: torch.nn.BatchNorm1d, bn2: torch.nn.BatchNorm1d) -> tuple:
+    """The ctn_tblock_params BatchNorm fields for a block's two nn.BatchNorm1d
+    (conv_tasnet.py:302-303), following torch.nn.modules.batchnorm._BatchNorm.forward:
+    a training-mode call counts num_batches_tracked and uses momentum (or the
+    cumulative factor 1/num_batches_tracked when momentum is None); batch statistics
+    are used in training mode or when there are no running statistics."""
+    training = bn1.training
+    out_ptrs, facs, epss = [], [], []
+    for bn in (bn1, bn2):
+        fac = 0.0 if bn.momentum is None else float(bn.momentum)
+        if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None:
+            bn.num_batches_tracked.add_(1)
+            if bn.momentum is None:
+                fac = 1.0 / float(bn.num_batches_tracked)
+        use_running = (not bn.training or bn.track_running_stats) and bn.running_mean is not None
+        for t in (bn.running_mean, bn.running_var):
+            if use_running and (t.dtype != torch.float32 or not t.is_contiguous()):
+                raise L.CtnLibraryError("BatchNorm running statistics must be contiguous float32")
+        out_ptrs += [bn.running_mean.data_ptr() if use_running else None,
+                     bn.running_var.data_ptr() if use_running else None]
+        facs.append(fac)
+        epss.append(float(bn.eps))
+    return (*out_ptrs, int(training), facs[0], facs[1], epss[0], epss[1])
+
+
 class TBlockFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, fr: Frames, cfg: tuple, pack, w1, a1, g1, b1, wd, a2, g2, b2, w2):
-        """pack: (w1s, w2s, w1t, w2t) bf16 copies from WeightPacks, or None."""
+    def forward(ctx, x, fr: Frames, cfg: tuple, pack, bn, w1, a1, g1, b1, wd, a2, g2, b2, w2):
+        """pack: (w1s, w2s, w1t, w2t) bf16 copies from WeightPacks, or None.
+        bn: BatchNorm state for norm_type BN (bn_state()), else None."""
         B, H, P, dil, causal, norm = cfg
         lib = L.load()
         L.require_device(x, "TemporalBlock")
@@ -91,7 +120,8 @@ class TBlockFn(torch.autograd.Function):
         desc = L.TBlockDesc(fr.M, fr.K, fr.Kp, B, H, P, dil, int(causal), norm, L.dtype_code(x.dtype))
         pack = pack if x.dtype == torch.bfloat16 else None
         ctx.pack = pack
-        pstruct = L.TBlockParams(*[p.data_ptr() for p in params], *(pack or (None,) * 4))
+        ctx.bn = bn or _NO_BN
+        pstruct = L.TBlockParams(*[p.data_ptr() for p in params], *(pack or (None,) * 4), *ctx.bn)
         y = torch.empty_like(x)
         h1 = x.new_empty(fr.rows, H)
         d = x.new_empty(fr.rows, H)
@@ -115,7 +145,7 @@ class TBlockFn(torch.autograd.Function):
         if gy.dtype != x.dtype:
             gy = gy.to(x.dtype)
         desc = L.TBlockDesc(*ctx.desc)
-        pstruct = L.TBlockParams(*[p.data_ptr() for p in params], *(ctx.pack or (None,) * 4))
+        pstruct = L.TBlockParams(*[p.data_ptr() for p in params], *(ctx.pack or (None,) * 4), *ctx.bn)
         saved = L.TBlockSaved(h1.data_ptr(), d.data_ptr(), stats.data_ptr())
         gx = torch.empty_like(x)
         grads = [torch.empty_like(p) for p in params]
@@ -126,7 +156,7 @@ class TBlockFn(torch.autograd.Function):
                                         ctypes.byref(saved), gy.data_ptr(), gx.data_ptr(), ctypes.byref(gstruct),
                                         ws.data_ptr(), nb, L.stream_handle(x.device)),
                 "ctn_tblock_backward")
-        return (gx, None, None, None, *grads)
+        return (gx, None, None, None, None, *grads)
 
 
 # ----------------------------------------------------------------------------

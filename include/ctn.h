@@ -32,10 +32,11 @@
 extern "C" {
 #endif
 
-#define CTN_ABI_VERSION 2
+#define CTN_ABI_VERSION 3
 
 typedef enum { CTN_DTYPE_F32 = 0, CTN_DTYPE_BF16 = 1 } ctn_dtype;
-typedef enum { CTN_NORM_GLN = 0, CTN_NORM_CLN = 1 } ctn_norm_type;
+/* CTN_NORM_BN: torch.nn.BatchNorm1d, chose_norm's fallback branch (conv_tasnet.py:302-303) */
+typedef enum { CTN_NORM_GLN = 0, CTN_NORM_CLN = 1, CTN_NORM_BN = 2 } ctn_norm_type;
 typedef enum { CTN_MASK_RELU = 0, CTN_MASK_SOFTMAX = 1 } ctn_mask_type;
 typedef enum {
   CTN_OK = 0,
@@ -81,6 +82,18 @@ typedef struct {            /* fp32 device pointers, reference shapes */
   const void* w2_bf16;
   const void* w1t_bf16;     /* [B][H] */
   const void* w2t_bf16;     /* [H][B] */
+  /* norm_type CTN_NORM_BN only (gamma/beta above = BatchNorm1d weight/bias, [H]):
+   * running statistics of net.2 and net.3.net.{2|3} (NULL: none, batch statistics
+   * always), updated in place by a training-mode forward with the unbiased batch
+   * variance; `bn_momentum` is torch's exponential factor (momentum, or
+   * 1/num_batches_tracked when momentum is None) */
+  float* bn_mean1;
+  float* bn_var1;
+  float* bn_mean2;
+  float* bn_var2;
+  int32_t bn_training;      /* 1: batch statistics (train mode), 0: running statistics */
+  float bn_momentum1, bn_momentum2;
+  float bn_eps1, bn_eps2;
 } ctn_tblock_params;
 
 /* One fp32 weight [rows][cols] -> bf16 copy (dst, same layout) and/or bf16
@@ -102,7 +115,7 @@ typedef struct {            /* fp32 outputs, same shapes as ctn_tblock_params */
 typedef struct {            /* forward results kept for backward */
   void* h1;                 /* [M*Kp, H] pre-PReLU output of the first 1x1 conv */
   void* d;                  /* [M*Kp, H] pre-PReLU output of the depthwise conv */
-  float* stats;             /* [4*G]: (mean,rstd) of norm1 then norm2; G = M (gLN) or M*Kp (cLN) */
+  float* stats;             /* [4*G]: (mean,rstd) of norm1 then norm2; G = M (gLN), M*Kp (cLN) or H (BN) */
 } ctn_tblock_saved;
 
 int ctn_tblock_stats_floats(const ctn_tblock_desc* d);

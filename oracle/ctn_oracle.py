@@ -161,12 +161,23 @@ def bn(y, weight, bias, training=True, running=None):
     return F.batch_norm(y, rm, rv, weight, bias, False, 0.0, 1e-5)
 
 
+# Test hook for BatchNorm running statistics: {norm prefix: (running_mean, running_var)}.
+# When set, BN follows nn.BatchNorm1d with its buffers: training mode (BN_TRAINING)
+# normalizes with batch statistics and updates the buffers in place (momentum 0.1,
+# unbiased variance); eval mode normalizes with the buffers.  None: batch statistics.
+BN_RUNNING = None
+BN_TRAINING = True
+
+
 def norm(cfg: Cfg, y, params, prefix):
     """chose_norm dispatch (conv_tasnet.py:292-303)."""
     if cfg.norm_type == "gLN":
         return gln(y, params[prefix + "gamma"], params[prefix + "beta"])
     if cfg.norm_type == "cLN":
         return cln(y, params[prefix + "gamma"], params[prefix + "beta"])
+    if BN_RUNNING is not None:
+        rm, rv = BN_RUNNING[prefix]
+        return F.batch_norm(y, rm, rv, params[prefix + "weight"], params[prefix + "bias"], BN_TRAINING, 0.1, 1e-5)
     return bn(y, params[prefix + "weight"], params[prefix + "bias"])
 
 

@@ -62,8 +62,11 @@ def test_tblock_validation(lib):
     assert lib.ctn_tblock_workspace_bytes(ctypes.byref(ok), 1) > lib.ctn_tblock_workspace_bytes(ctypes.byref(ok), 0)
     assert lib.ctn_tblock_stats_floats(ctypes.byref(ok)) == 4 * 2
     assert lib.ctn_tblock_stats_floats(ctypes.byref(_desc(norm_type=1))) == 4 * 2 * 3200
+    bn = _desc(norm_type=2)                         # BatchNorm: per-channel statistics
+    assert lib.ctn_tblock_stats_floats(ctypes.byref(bn)) == 4 * bn.H
+    assert lib.ctn_tblock_workspace_bytes(ctypes.byref(bn), 1) > 0
+    assert lib.ctn_tblock_workspace_bytes(ctypes.byref(_desc(norm_type=3)), 0) == 0
     cases = [(_desc(Kp=3199), L.CtnLibraryError, "multiple of 128"),
-             (_desc(norm_type=2), None, "BN"),
              (_desc(P=2), None, "odd P"),
              (_desc(B=100), None, "multiples of 8")]
     for d, _, msg in cases:

@@ -59,7 +59,7 @@ def run(model, g, bf16=False):
 
 
 MODELS = ["model_c1.npz", "model_paper_short.npz", "model_causal_cln.npz", "model_3spk.npz",
-          "model_softmax_pad.npz"]
+          "model_softmax_pad.npz", "model_bn.npz"]
 
 
 @pytest.mark.parametrize("name", MODELS)
@@ -119,13 +119,68 @@ def test_model_bf16_sisnri_within_0p1db(name):
             assert rel(gr, g["g:" + n].reshape(-1)) < 0.1, n
 
 
-def test_bn_is_reported_unsupported():
-    import ctn_lib as L
+def _bn_modules(model):
+    """(oracle norm prefix, nn.BatchNorm1d) of every TemporalBlock norm."""
+    out = []
+    for r, rep in enumerate(model.separator.network[2]):
+        for xi, blk in enumerate(rep):
+            n1, n2 = blk._norms()
+            off = 1 if blk._geo[4] else 0
+            p = O.block_prefix(r, xi)
+            out += [(p + "net.2.", n1), (p + f"net.3.net.{2 + off}.", n2)]
+    return out
+
+
+def test_bn_running_statistics_and_eval_mode():
+    """BatchNorm1d blocks (norm_type "BN", conv_tasnet.py:302-303): a training-mode
+    forward updates running_mean / running_var (momentum 0.1, unbiased variance) and
+    num_batches_tracked as torch does; an eval-mode forward normalizes with them.
+    Checked against the fp32 oracle run with nn.BatchNorm1d buffer semantics."""
     g = load("model_bn.npz")
     cfg = cfg_of(g)
     model = build(cfg, g)
-    with pytest.raises(L.CtnLibraryError):
-        model(T(g["mix"]))
+    mix = T(g["mix"])
+    with torch.no_grad():
+        model(mix)                                    # training mode
+    mods = _bn_modules(model)
+    params = {n: torch.from_numpy(g["p:" + n]) for n, _ in O.param_shapes(cfg)}
+    running = {p: (torch.zeros(m.num_features), torch.ones(m.num_features)) for p, m in mods}
+    try:
+        O.BN_RUNNING, O.BN_TRAINING = running, True
+        O.model_forward(cfg, torch.from_numpy(g["mix"]), params)
+        for p, m in mods:
+            assert int(m.num_batches_tracked) == 1
+            np.testing.assert_allclose(m.running_mean.cpu().numpy(), running[p][0].numpy(), rtol=1e-4, atol=1e-5,
+                                       err_msg=p)
+            np.testing.assert_allclose(m.running_var.cpu().numpy(), running[p][1].numpy(), rtol=1e-4, atol=1e-5,
+                                       err_msg=p)
+        model.eval()
+        with torch.no_grad():
+            est = model(mix)
+        O.BN_TRAINING = False
+        ref = O.model_forward(cfg, torch.from_numpy(g["mix"]), params)
+    finally:
+        O.BN_RUNNING, O.BN_TRAINING = None, True
+    assert rel(est.cpu().numpy(), ref.numpy()) < 1e-4
+    for p, m in mods:                                 # eval mode leaves the buffers alone
+        assert int(m.num_batches_tracked) == 1
+
+
+def test_bn_bf16_training_step():
+    """bf16 activations through the BN path: the estimate stays within 5e-2 relative
+    L2 of the fp32 reference and every gradient is finite with the reference norm
+    to 10 % (the bf16 bar of test_model_bf16_sisnri_within_0p1db)."""
+    g = load("model_bn.npz")
+    cfg = cfg_of(g)
+    model = build(cfg, g)
+    est, loss, max_snr, reord = run(model, g, bf16=True)
+    assert rel(est.detach().cpu().numpy(), g["est"]) < 5e-2
+    params = dict(model.named_parameters())
+    for n, shape in O.param_shapes(cfg):
+        gr = params[n].grad.detach().cpu().reshape(-1).numpy()
+        assert np.isfinite(gr).all(), n
+        if len(shape) >= 2:
+            assert abs(np.linalg.norm(gr) / float(g["gnorm:" + n]) - 1) < 0.1, n
 
 
 @pytest.mark.parametrize("L_", [20, 16])

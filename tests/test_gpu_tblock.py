@@ -30,7 +30,7 @@ def run_block(x_ncw, params, P, dil, causal, norm, G_ncw, dtype=torch.float32):
     x = ops.ncw_to_rows(x_ncw.to(DEV), fr, dtype).requires_grad_(True)
     ps = [p.to(DEV).float().clone().requires_grad_(True) for p in params]
     cfg = (B, H, P, dil, causal, L.NORM_GLN if norm == "gLN" else L.NORM_CLN)
-    y = ops.TBlockFn.apply(x, fr, cfg, None, *ps)
+    y = ops.TBlockFn.apply(x, fr, cfg, None, None, *ps)
     y_ncw = ops.rows_to_ncw(y, fr, torch.float32)
     (y_ncw * G_ncw.to(DEV)).sum().backward()
     gx = ops.rows_to_ncw(x.grad, fr, torch.float32)
@@ -126,7 +126,7 @@ def test_weight_packs_match_per_call_conversion():
         for p in ps:
             p.grad = None
         xx = x.clone().requires_grad_(True)
-        y = ops.TBlockFn.apply(xx, fr, cfg, pack, *ps)
+        y = ops.TBlockFn.apply(xx, fr, cfg, pack, None, *ps)
         y.float().square().sum().backward()
         return y.detach(), xx.grad.detach(), [p.grad.detach().clone() for p in ps]
 
