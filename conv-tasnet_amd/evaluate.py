@@ -14,9 +14,10 @@ Same flags and printout as the reference.  Differences, each deliberate:
   assigned to it; the reference's reorder_source uses the permutation itself,
   which mis-pairs 3-cycles for C >= 3 (pit_criterion.py:91-97).  Default 0 keeps
   the reference's pairing (identical for C = 2);
-* SDRi needs mir_eval's bss_eval_sources (evaluate.py:10,90-105), which is not
-  installed in this image: ``--cal_sdr 1`` raises unless mir_eval is importable
-  (SDRi parity is unpinned).
+* SDRi uses mir_eval's bss_eval_sources (evaluate.py:10,90-105) when it is
+  importable and otherwise ``bss_eval.bss_eval_sources``, a from-scratch
+  restatement of the same BSS Eval v3 algorithm (mir_eval is not installed in
+  this image, so SDRi parity is unpinned).
 """
 import argparse
 
@@ -105,9 +106,8 @@ def cal_SDRi(src_ref, src_est, mix):
     """evaluate.py:90-105 (C speakers): mean over sources of SDR(est) - SDR(mixture)."""
     try:
         from mir_eval.separation import bss_eval_sources
-    except ImportError as e:
-        raise RuntimeError("SDRi needs mir_eval.separation.bss_eval_sources, which is not installed; "
-                           "run without --cal_sdr") from e
+    except ImportError:          # this image: the from-scratch BSS Eval v3 (parity unpinned)
+        from bss_eval import bss_eval_sources
     src_anchor = np.stack([mix] * src_ref.shape[0], axis=0)
     sdr, sir, sar, popt = bss_eval_sources(src_ref, src_est)
     sdr0, sir0, sar0, popt0 = bss_eval_sources(src_ref, src_anchor)
