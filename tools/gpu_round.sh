@@ -14,6 +14,7 @@ timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 tail -1 $O/smoke.log
 timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/$O/pmc/p1 -o run -- python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 > $O/pmc1.log 2>&1
 timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/$O/pmc/p2 -o run -- python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 > $O/pmc2.log 2>&1
+# the JSON lands in profiles/ on the box only: copy $O/traffic.log to profiles/pmc_traffic.json here
 python tools/pmc_traffic.py $O/pmc profiles/pmc_traffic.json > $O/traffic.log
 echo PMC done
 timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err
