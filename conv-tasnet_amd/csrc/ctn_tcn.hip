@@ -18,10 +18,17 @@
 
 namespace ctn {
 
+#ifndef CTN_DW_PF
+#define CTN_DW_PF 2
+#endif
 constexpr int DW_RPB = 128;   // rows per workgroup (element-wise kernels)
 constexpr int DW_MAXP = 8;
 constexpr int DW_MINSEG = 16; // shortest comb segment (halo rows cost (P-1)/seg)
 constexpr int DW_WPS_FWD = 4, DW_WPS_BWD = 2;   // waves/SIMD the kernels' VGPR budgets allow
+// comb rows prefetched per lane: 2 for bf16 (the loop is latency-bound at one row
+// in flight: 8 waves x 48 B per lane per CU is half of what Little's law asks at
+// 6 TB/s), 1 for fp32 (parity mode; two would exceed the VGPR budgets above)
+template <typename T> constexpr int dw_pf() { return sizeof(T) == 2 ? CTN_DW_PF : 1; }
 
 // ---------------------------------------------------------------------------
 // Comb decomposition of the dilated depthwise conv.  Rows of one utterance are
@@ -167,12 +174,21 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
     fetch(it.j0 + i - POWN, r, ok, row);
     finish(r, ok, row, win[i]);
   }
-  Raw8<T> pre; bool pok; int prow;
-  fetch(it.j0 + P - 1 - POWN, pre, pok, prow);
+  // DW_PF rows in flight per lane: slot q holds comb step j with j % DW_PF == q,
+  // and the loop is unrolled by DW_PF so a slot is refilled (step j + DW_PF) as
+  // soon as it is consumed, without register copies that would wait on a load.
+  constexpr int D = dw_pf<T>();
+  Raw8<T> pre[D]; bool pok[D]; int prow[D];
+#pragma unroll
+  for (int q = 0; q < D; ++q) fetch(it.j0 + q + P - 1 - POWN, pre[q], pok[q], prow[q]);
   float ts = 0.f, tss = 0.f;
-  for (int j = it.j0; j < it.j1; ++j) {
-    Raw8<T> cur = pre; const bool cok = pok; const int crow = prow;
-    if (j + 1 < it.j1) fetch(j + P - POWN, pre, pok, prow);
+  for (int jb = it.j0; jb < it.j1; jb += D)
+#pragma unroll
+  for (int q = 0; q < D; ++q) {
+    const int j = jb + q;
+    if (j >= it.j1) break;
+    Raw8<T> cur = pre[q]; const bool cok = pok[q]; const int crow = prow[q];
+    if (j + D < it.j1) fetch(j + D + P - 1 - POWN, pre[q], pok[q], prow[q]);
     finish(cur, cok, crow, win[P - 1]);
     const int k = row_of(j);
     float out[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -310,16 +326,24 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
     finish_h(rh, rowh, ahw[i]);
     ahok[i] = okh;
   }
-  Raw8<T> pd, pg, ph; bool pok, pokh; int prow, prowh;
-  fetch_g(it.j0 + GT, pd, pg, pok, prow);
-  fetch_h(it.j0 + AT, ph, pokh, prowh);
-  for (int j = it.j0; j < it.j1; ++j) {
-    Raw8<T> cd = pd, cgv = pg, ch = ph;
-    const bool cok = pok, cokh = pokh;
-    const int crow = prow, crowh = prowh;
-    if (j + 1 < it.j1) {
-      fetch_g(j + 1 + GT, pd, pg, pok, prow);
-      fetch_h(j + 1 + AT, ph, pokh, prowh);
+  constexpr int D = dw_pf<T>();   // rows in flight per lane, slots as in dw_fwd
+  Raw8<T> pd[D], pg[D], ph[D]; bool pok[D], pokh[D]; int prow[D], prowh[D];
+#pragma unroll
+  for (int q = 0; q < D; ++q) {
+    fetch_g(it.j0 + q + GT, pd[q], pg[q], pok[q], prow[q]);
+    fetch_h(it.j0 + q + AT, ph[q], pokh[q], prowh[q]);
+  }
+  for (int jb = it.j0; jb < it.j1; jb += D)
+#pragma unroll
+  for (int q = 0; q < D; ++q) {
+    const int j = jb + q;
+    if (j >= it.j1) break;
+    Raw8<T> cd = pd[q], cgv = pg[q], ch = ph[q];
+    const bool cok = pok[q], cokh = pokh[q];
+    const int crow = prow[q], crowh = prowh[q];
+    if (j + D < it.j1) {
+      fetch_g(j + D + GT, pd[q], pg[q], pok[q], prow[q]);
+      fetch_h(j + D + AT, ph[q], pokh[q], prowh[q]);
     }
     finish_g(cd, cgv, cok, crow, j + GT < it.j1, gdw[P - 1]);   // halo rows are counted by their own segment
     finish_h(ch, crowh, ahw[P - 1]);
