@@ -36,6 +36,14 @@ BF16_PEAK_TFLOPS = 2500.0      # dense bf16 MFMA
 
 PAPER = dict(N=256, L=20, B=256, H=512, P=3, X=8, R=4, C=2, norm_type="gLN", causal=False,
              mask_nonlinear="relu")
+# BASELINE.json configs runnable on one GPU: c2 is the metric's workload (the
+# default); c4 (causal cLN, L=16, 16 kHz) and c5 (3 speakers, N=512, 8 s) are
+# measured per GPU at their per-GPU batch for the record, never as the bench line.
+CONFIGS = {
+    "c2": (PAPER, 8000, 4.0, 32),
+    "c4": (dict(PAPER, L=16, norm_type="cLN", causal=True), 16000, 4.0, 64),
+    "c5": (dict(PAPER, N=512, C=3), 8000, 8.0, 16),
+}
 
 # timer kinds (include/ctn.h ctn_timer_enable)
 TIMER_GEMM1, TIMER_DW_FWD, TIMER_GEMM_BWD_A = 1, 2, 3
@@ -98,8 +106,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=32, help="utterances per GPU")
-    ap.add_argument("--seconds", type=float, default=4.0)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="c2",
+                    help="BASELINE.json config (c2 = the metric's workload)")
+    ap.add_argument("--batch", type=int, default=None, help="utterances per GPU (config default)")
+    ap.add_argument("--seconds", type=float, default=None, help="utterance length (config default)")
     ap.add_argument("--fp32", action="store_true", help="fp32 activations (parity mode) instead of bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--timer-kind", type=int, default=TIMER_GEMM_BWD_A)
@@ -119,9 +129,13 @@ def main():
     import pit_criterion as pc
     import synthetic
 
-    cfg = PAPER
+    cfg, rate, secs, batch = CONFIGS[args.config]
+    if args.config != "c2":
+        args.no_cpu_baseline = True   # the CPU baseline leg times the c2 workload only
+    args.batch = batch if args.batch is None else args.batch
+    args.seconds = secs if args.seconds is None else args.seconds
     M, C = args.batch, cfg["C"]
-    T = int(args.seconds * 8000)
+    T = int(args.seconds * rate)
     K = (T - cfg["L"]) // (cfg["L"] // 2) + 1
 
     torch.manual_seed(0)
@@ -195,8 +209,13 @@ def main():
             "vs_baseline": None,
             "dtype": "fp32" if args.fp32 else "bf16",
             "data": "synthetic (AR(2) speech-like sources, random-init weights)",
-            "config": {"workload": "paper config train step c2: N=256 L=20 B=256 H=512 P=3 X=8 R=4 gLN "
-                                   "non-causal relu-mask, 2 spk, 4 s @ 8 kHz, fwd+PIT loss+bwd+clip+Adam",
+            "config": {"workload": ("paper config train step c2: N=256 L=20 B=256 H=512 P=3 X=8 R=4 gLN "
+                                    "non-causal relu-mask, 2 spk, 4 s @ 8 kHz, fwd+PIT loss+bwd+clip+Adam"
+                                    if args.config == "c2" else
+                                    f"{args.config} train step: N={cfg['N']} L={cfg['L']} B={cfg['B']} H={cfg['H']} "
+                                    f"P={cfg['P']} X={cfg['X']} R={cfg['R']} {cfg['norm_type']} "
+                                    f"{'causal' if cfg['causal'] else 'non-causal'} relu-mask, {C} spk, "
+                                    f"{args.seconds:g} s @ {rate // 1000} kHz, fwd+PIT loss+bwd+clip+Adam"),
                        "per_gpu_batch": M, "global_batch": M * world, "samples": T, "frames": K,
                        "parallelism": f"dp{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
