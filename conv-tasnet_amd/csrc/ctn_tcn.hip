@@ -578,7 +578,10 @@ __global__ __launch_bounds__(256) void stats_finalize_block_kernel(const double2
 
 hipError_t launch_stats_finalize(const double2* slab, int G, int nparts, double cnt, int mode, float eps,
                                  float2* out, hipStream_t s) {
-  if (nparts >= 8)
+  // one workgroup per group only when groups are few and long (gLN: one per
+  // utterance); cLN has a group per frame row (G = M*Kp, 516k at c4), where a
+  // workgroup per row cost 540 us per launch against a few us for a thread per row
+  if (nparts >= 8 && (G < 8192 || nparts > 64))
     hipLaunchKernelGGL(stats_finalize_block_kernel, dim3(G), dim3(256), 0, s, slab, nparts, cnt, mode, eps, out);
   else
     hipLaunchKernelGGL(stats_finalize_thread_kernel, dim3((G + 255) / 256), dim3(256), 0, s, slab, G, nparts, cnt,
