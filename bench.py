@@ -80,14 +80,37 @@ def step_flops(M, K, cfg):
     return 3 * f * M
 
 
-def cpu_baseline(seconds=15.0):
-    """fp32 CPU oracle train step (fwd + loss + bwd + clip + Adam) on the paper config, M=1."""
+def _cpu_model():
+    """CPU model name and the physical cores this process may run on (lscpu's view)."""
+    name, cores = "unknown", set()
+    try:
+        with open("/proc/cpuinfo") as f:
+            phys = core = None
+            for line in f:
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "model name" and name == "unknown":
+                    name = v
+                elif k == "physical id":
+                    phys = v
+                elif k == "core id":
+                    core = v
+                elif not k and phys is not None:
+                    cores.add((phys, core))
+                    phys = core = None
+    except OSError:
+        pass
+    allowed = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    return name, len(cores) or None, allowed
+
+
+def _time_train_steps(cfg_d, T, seconds):
     from oracle import ctn_oracle as O
     import synthetic
-    cfg = O.Cfg(**{k: PAPER[k] for k in ("N", "L", "B", "H", "P", "X", "R", "C")})
+    cfg = O.Cfg(**{k: cfg_d[k] for k in ("N", "L", "B", "H", "P", "X", "R", "C")})
     params = O.init_params(cfg, 0)
-    mix, src = synthetic.speech_like(1, cfg.C, 32000, 99)
-    lens = torch.tensor([32000])
+    mix, src = synthetic.speech_like(1, cfg.C, T, 99)
+    lens = torch.tensor([T])
     O.train_step(cfg, params, mix, src, lens)                 # warm-up
     n, t0 = 0, time.perf_counter()
     while True:
@@ -95,10 +118,23 @@ def cpu_baseline(seconds=15.0):
         n += 1
         el = time.perf_counter() - t0
         if el >= seconds:
-            break
-    return {"value": n / el, "unit": "utterances/sec", "cores": torch.get_num_threads(), "kind": "port",
+            return n, el
+
+
+def cpu_baseline(seconds=12.0):
+    """fp32 CPU oracle train step (fwd + loss + bwd + clip + Adam), M=1, on this box's host
+    cores: the paper config (the reported value) and c1 (BASELINE.json configs[0])."""
+    threads = torch.get_num_threads()
+    name, phys, allowed = _cpu_model()
+    n, el = _time_train_steps(PAPER, 32000, seconds)
+    n1, el1 = _time_train_steps(dict(PAPER, N=64, B=64, H=128, X=2, R=2), 32000, seconds / 3)
+    return {"value": n / el, "unit": "utterances/sec", "cores": threads, "kind": "port",
+            "cpu": name, "physical_cores_on_host": phys, "cpus_allowed": allowed,
             "sample": f"{n} training steps (fwd+PIT loss+bwd+clip+Adam) of 1 utterance, paper config, "
-                      f"4 s @ 8 kHz, fp32 oracle/ctn_oracle.py, {el:.1f} s"}
+                      f"4 s @ 8 kHz, fp32 oracle/ctn_oracle.py on {threads} threads, {el:.1f} s",
+            "c1": {"value": n1 / el1, "unit": "utterances/sec",
+                   "sample": f"{n1} c1 training steps (N=64 B=64 H=128 X=2 R=2), 1 utterance 4 s @ 8 kHz, "
+                             f"{el1:.1f} s"}}
 
 
 def main():
@@ -113,12 +149,15 @@ def main():
     ap.add_argument("--fp32", action="store_true", help="fp32 activations (parity mode) instead of bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--timer-kind", type=int, default=TIMER_GEMM_BWD_A)
+    ap.add_argument("--ddp", action="store_true",
+                    help="DDP over RCCL even at world size 1 (exercises process-group init, bucket hooks)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    use_ddp = world > 1 or args.ddp
+    if use_ddp:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
@@ -141,7 +180,7 @@ def main():
     torch.manual_seed(0)
     model = ct.ConvTasNet(**cfg).to(dev)
     model.act_dtype = torch.float32 if args.fp32 else torch.bfloat16
-    if world > 1:
+    if use_ddp:
         model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], bucket_cap_mb=25)
     # the solver's update (src/solver.py:184-186) on the HIP path: one launch for
     # the clip norm, one for the clip scale, one for Adam over all 294 tensors
@@ -164,21 +203,21 @@ def main():
     torch.cuda.synchronize(dev)
     lib = L.load()
     L.check(lib.ctn_timer_enable(args.timer_kind, args.steps * 64), "ctn_timer_enable")
-    if world > 1:
+    if use_ddp:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if use_ddp:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     tot = ctypes.c_double(0.0)
     nl = ctypes.c_int(0)
     L.check(lib.ctn_timer_read(ctypes.byref(tot), ctypes.byref(nl)), "ctn_timer_read")
     lib.ctn_timer_enable(0, 0)
-    if world > 1:
+    if use_ddp:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
@@ -217,7 +256,7 @@ def main():
                                     f"{'causal' if cfg['causal'] else 'non-causal'} relu-mask, {C} spk, "
                                     f"{args.seconds:g} s @ {rate // 1000} kHz, fwd+PIT loss+bwd+clip+Adam"),
                        "per_gpu_batch": M, "global_batch": M * world, "samples": T, "frames": K,
-                       "parallelism": f"dp{world}"},
+                       "parallelism": f"dp{world}" + (" (DDP/RCCL)" if use_ddp else "")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": {1: "gemm_rows fwd 1x1 B->H (PReLU-stats epilogue)",
@@ -234,7 +273,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_ddp:
         dist.destroy_process_group()
 
 

@@ -86,7 +86,7 @@ class ConvTasNet(nn.Module):
         packs = [None] * len(blocks)
         if dt == torch.bfloat16:   # bf16 weight copies for every block: one launch per step
             if not hasattr(self, "_packs"):
-                self._packs = ops.WeightPacks()
+                self._packs = ops.PackCache()
             packs = self._packs.get([(b.net[0].weight, b._params()[8]) for b in blocks], mixture.device)
         for blk, pk in zip(blocks, packs):
             x = blk._forward_rows(x, fr, norm, pk)

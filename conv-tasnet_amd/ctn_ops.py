@@ -51,7 +51,10 @@ class WeightPacks:
         self.ptrs = []
 
     def get(self, pairs: list, device) -> list:
-        """pairs: [(w1, w2)] fp32 parameters -> [(w1s, w2s, w1t, w2t) device pointers]."""
+        """pairs: [(w1, w2)] fp32 parameters -> [(w1s, w2s, w1t, w2t, buf)]: four device
+        pointers into ``buf``, returned WITH the buffer so that every autograd node
+        that saves a pack keeps its storage alive until its backward has run (the
+        cache may reallocate ``buf`` between forward and backward)."""
         key = (device, tuple((w1.data_ptr(), w2.data_ptr(), tuple(w1.shape), tuple(w2.shape)) for w1, w2 in pairs))
         if key != self.key:
             sizes = [(w1.numel(), w2.numel()) for w1, w2 in pairs]
@@ -76,7 +79,23 @@ class WeightPacks:
         if packs:
             arr = (L.WeightPack * len(packs))(*packs)
             L.check(L.load().ctn_pack_weights(arr, len(packs), L.stream_handle(device)), "ctn_pack_weights")
-        return self.ptrs
+        return [(*p, self.buf) for p in self.ptrs]
+
+
+class PackCache:
+    """One WeightPacks per device.  nn.DataParallel replicas share their module's
+    __dict__ (src/train.py:121 replicates per forward), so a single shared cache
+    would be re-keyed and overwritten concurrently by the per-GPU threads; keyed by
+    device, each thread only ever touches its own entry."""
+
+    def __init__(self):
+        self.by_dev = {}
+
+    def get(self, pairs: list, device) -> list:
+        wp = self.by_dev.get(device)
+        if wp is None:
+            wp = self.by_dev.setdefault(device, WeightPacks())
+        return wp.get(pairs, device)
 
 
 _NO_BN = (None, None, None, None, 0, 0.0, 0.0, 0.0, 0.0)
@@ -119,9 +138,9 @@ class TBlockFn(torch.autograd.Function):
         params = [_f32(t) for t in (w1, a1, g1, b1, wd, a2, g2, b2, w2)]
         desc = L.TBlockDesc(fr.M, fr.K, fr.Kp, B, H, P, dil, int(causal), norm, L.dtype_code(x.dtype))
         pack = pack if x.dtype == torch.bfloat16 else None
-        ctx.pack = pack
+        ctx.pack = pack          # (4 pointers, buf): keeps the packed storage alive until backward
         ctx.bn = bn or _NO_BN
-        pstruct = L.TBlockParams(*[p.data_ptr() for p in params], *(pack or (None,) * 4), *ctx.bn)
+        pstruct = L.TBlockParams(*[p.data_ptr() for p in params], *(pack[:4] if pack else (None,) * 4), *ctx.bn)
         y = torch.empty_like(x)
         h1 = x.new_empty(fr.rows, H)
         d = x.new_empty(fr.rows, H)
@@ -145,7 +164,8 @@ class TBlockFn(torch.autograd.Function):
         if gy.dtype != x.dtype:
             gy = gy.to(x.dtype)
         desc = L.TBlockDesc(*ctx.desc)
-        pstruct = L.TBlockParams(*[p.data_ptr() for p in params], *(ctx.pack or (None,) * 4), *ctx.bn)
+        pstruct = L.TBlockParams(*[p.data_ptr() for p in params], *(ctx.pack[:4] if ctx.pack else (None,) * 4),
+                                 *ctx.bn)
         saved = L.TBlockSaved(h1.data_ptr(), d.data_ptr(), stats.data_ptr())
         gx = torch.empty_like(x)
         grads = [torch.empty_like(p) for p in params]

@@ -124,16 +124,23 @@ class AudioDataLoader(data.DataLoader):
 
 
 class MinibatchSampler(torch.utils.data.Sampler):
-    """Rank `rank` of `world` takes order[rank::world] of the first
-    world * (n // world) minibatches, so every rank runs the same number of
-    steps; with shuffle the order is a permutation seeded by (seed + epoch),
-    identical on all ranks (call set_epoch each epoch)."""
+    """Rank `rank` of `world` takes order[rank::world] of the minibatches; with
+    shuffle the order is a permutation seeded by (seed + epoch), identical on all
+    ranks (call set_epoch each epoch).
 
-    def __init__(self, dataset, rank=0, world=1, shuffle=False, seed=0):
+    drop_last=True (training): only the first world * (n // world) minibatches are
+    used, so every rank runs the same number of DDP steps.  drop_last=False
+    (validation): every minibatch is used, the low ranks taking the remainder, so
+    the cross-validation loss that drives LR halving / early stopping sees the
+    whole set (the solver all-reduces (sum, count) pairs, so unequal shards are
+    fine there)."""
+
+    def __init__(self, dataset, rank=0, world=1, shuffle=False, seed=0, drop_last=True):
         if not 0 <= rank < world:
             raise ValueError(f"rank {rank} outside world size {world}")
         self.n, self.rank, self.world = len(dataset), rank, world
         self.shuffle, self.seed, self.epoch = bool(shuffle), seed, 0
+        self.drop_last = bool(drop_last)
 
     def set_epoch(self, epoch):
         self.epoch = int(epoch)
@@ -146,11 +153,15 @@ class MinibatchSampler(torch.utils.data.Sampler):
         return list(range(self.n))
 
     def __iter__(self):
-        order = self._order()[:(self.n // self.world) * self.world]
+        order = self._order()
+        if self.drop_last:
+            order = order[:(self.n // self.world) * self.world]
         return iter(order[self.rank::self.world])
 
     def __len__(self):
-        return self.n // self.world
+        if self.drop_last:
+            return self.n // self.world
+        return len(range(self.rank, self.n, self.world))
 
 
 def _collate_fn(batch):

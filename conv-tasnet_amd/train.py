@@ -144,7 +144,7 @@ def main(args):
                                 sampler=MinibatchSampler(tr_dataset, rank, world, shuffle=args.shuffle),
                                 num_workers=args.num_workers)
     cv_loader = AudioDataLoader(cv_dataset, batch_size=1,
-                                sampler=MinibatchSampler(cv_dataset, rank, world), num_workers=0)
+                                sampler=MinibatchSampler(cv_dataset, rank, world, drop_last=False), num_workers=0)
     data = {'tr_loader': tr_loader, 'cv_loader': cv_loader}
     # model
     model = ConvTasNet(args.N, args.L, args.B, args.H, args.P, args.X, args.R,

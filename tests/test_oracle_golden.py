@@ -177,3 +177,22 @@ def test_reference_init_semantics():
             assert np.all(p == 0.25), n
         elif n.endswith("gamma"):
             assert not np.allclose(p, 1.0), n
+
+
+def test_trained_model_fixture():
+    """The oracle reproduces the reference's output and per-utterance SI-SNRi on the
+    weights the reference trained (tests/golden/make_golden_trained.py)."""
+    g = load("model_trained_c1.npz")
+    N, L_, B, H, P, X, R, C = [int(v) for v in g["cfg"]]
+    cfg = O.Cfg(N, L_, B, H, P, X, R, C)
+    params = {n: T(g["p:" + n]) for n, _ in O.param_shapes(cfg)}
+    with torch.no_grad():
+        est = O.model_forward(cfg, T(g["mix"]), params)
+        loss, _, est_m, reord = O.cal_loss(T(g["src"]), est, T(g["len"]))
+    scale = float(np.abs(g["est"]).max())
+    close(est_m, g["est"], 1e-4, 1e-5 * scale)
+    close(float(loss), float(g["loss"]), 1e-5, 1e-5)
+    for b in range(est.shape[0]):
+        l = int(g["len"][b])
+        v = O.cal_sisnri(g["src"][b, :, :l], reord[b, :, :l].numpy(), g["mix"][b, :l])
+        assert abs(v - g["sisnri"][b]) < 1e-3

@@ -193,6 +193,11 @@ def test_minibatch_sampler_shards():
     assert list(a) != first
     with pytest.raises(ValueError):
         data.MinibatchSampler(ds, 4, 4)
+    # validation shards keep every minibatch (the low ranks take the remainder)
+    cv = [list(data.MinibatchSampler(ds, r, 4, drop_last=False)) for r in range(4)]
+    assert [len(s) for s in cv] == [6, 6, 6, 5]
+    assert [len(data.MinibatchSampler(ds, r, 4, drop_last=False)) for r in range(4)] == [6, 6, 6, 5]
+    assert sorted(sum(cv, [])) == list(range(23))
 
 
 # ---------------------------------------------------------------- evaluation metric
