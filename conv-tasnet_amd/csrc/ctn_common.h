@@ -11,6 +11,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+#include <utility>
+
 #define CTN_DEV __device__ __forceinline__
 
 typedef uint16_t bf16raw;
@@ -314,3 +317,11 @@ template <int NK> CTN_DEV int stat_index(int row, int Kp) {
 }
 
 static inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
+
+// Compile-time loop: f(std::integral_constant<int, i>{}) for i = 0 .. N-1, so that
+// register-array indices derived from i stay static (register rings unrolled by
+// their depth).
+template <class F, int... I> CTN_DEV void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F> CTN_DEV void static_for(F&& f) { static_for_impl(f, std::make_integer_sequence<int, N>{}); }

@@ -42,6 +42,36 @@ constexpr int WS_FOLD_MAX = 512;   // utterances whose gLN operand stats a workg
 #ifndef CTN_WS_EXP
 #define CTN_WS_EXP 0
 #endif
+// A-tile register ring depth (tiles whose loads are in flight while one is staged)
+// of the 16-wave and 8-wave non-interleaved configurations
+#ifndef CTN_WS_PF16
+#define CTN_WS_PF16 1
+#endif
+#ifndef CTN_WS_PF8
+#define CTN_WS_PF8 1
+#endif
+// Issue order inside a tile iteration of the non-interleaved configurations.
+// gfx9 retires loads and stores in one in-order vmcnt queue, so a load issued
+// behind a tile's output stores cannot be consumed before those stores are
+// acknowledged.  1: stage(t+1) and the loads of the next tiles go BEFORE the output
+// stores of tile t (which are written last); 0: the original order (stores, then
+// the next loads).
+// Output-channel slices of the Nout = 512 forward GEMM: 2 = two independent
+// 8-wave workgroups per CU, each holding half the weight (the A tile is read by
+// both from the XCD's L2), instead of one 16-wave workgroup.
+#ifndef CTN_WS_S512
+#define CTN_WS_S512 1
+#endif
+// LDS fragment look-ahead of the MFMA loop, in k-steps
+#ifndef CTN_WS_LA16
+#define CTN_WS_LA16 1
+#endif
+#ifndef CTN_WS_LA8
+#define CTN_WS_LA8 3
+#endif
+#ifndef CTN_WS_ORDER
+#define CTN_WS_ORDER 1
+#endif
 
 // LDS byte offset of the 16-byte piece (frame row lr, k-chunk lg) of k-block kb
 // in fragment order: ds_read_b128 groups and ds_write_b128 groups both hit
@@ -55,8 +85,11 @@ CTN_DEV void ready(const v4u& v) { asm volatile("" ::"v"(v)); }
 CTN_DEV void ready(float v) { asm volatile("" ::"v"(v)); }
 
 
-template <int OPK, int NK, int EPI, int NB, int KB, int WV, int MB>
-__global__ __launch_bounds__(64 * WV) void gemm_ws_kernel(GemmRows p) {
+// S: output-channel slices; workgroup b -> (row range rr, slice sl), the S slices of
+// a range on one XCD (hardware ids are dealt round-robin over the 8 XCDs) so the A
+// tile comes from HBM once.  Each slice-workgroup holds NS = WV*16*NB channels.
+template <int OPK, int NK, int EPI, int NB, int KB, int WV, int MB, int S = 1>
+__global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p) {
   constexpr int NT = 64 * WV;                  // threads
   constexpr int TM = 16 * MB;                  // frame rows per tile
   constexpr int KR = KB * 32;                  // reduction length
@@ -70,6 +103,7 @@ __global__ __launch_bounds__(64 * WV) void gemm_ws_kernel(GemmRows p) {
   // one-tile register prefetch + two accumulator sets only where registers allow
   constexpr bool N1B = OPK == OP_NORM1_BWD;    // norm-1/PReLU-1 backward on the operand
   constexpr bool SWP = OPK == OP_PLAIN && WV == 8;
+  constexpr int PF = SWP ? 1 : (WV == 16 ? CTN_WS_PF16 : CTN_WS_PF8);
   __shared__ __attribute__((aligned(16))) char sA[2][TM * KR * 2];
   __shared__ float sgam[EPI == EPI_NORM_BWD ? NB * 16 * WV : 1];
   // gLN operand statistics, one pair per utterance, finalized here (StatFold)
@@ -81,11 +115,27 @@ __global__ __launch_bounds__(64 * WV) void gemm_ws_kernel(GemmRows p) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
   const int ntile = (int)(p.g.rows() / TM);
-  const int t0 = (int)((long)ntile * blockIdx.x / gridDim.x), t1 = (int)((long)ntile * (blockIdx.x + 1) / gridDim.x);
+  constexpr int NS = WV * 16 * NB;             // output channels per slice
+  const int nr = (int)gridDim.x / S;           // row ranges
+  int rr = (int)blockIdx.x, sl = 0;
+  if constexpr (S > 1) {
+    const int b = (int)blockIdx.x;
+    if (nr % 8 == 0) {
+      const int l = b / 8;
+      sl = l % S;
+      rr = (b % 8) * (nr / 8) + l / S;
+    } else {
+      sl = b % S;
+      rr = b / S;
+    }
+  }
+  const int t0 = (int)((long)ntile * rr / nr), t1 = (int)((long)ntile * (rr + 1) / nr);
   const int Kp = p.g.Kp, Kv = p.g.K;
   const bf16raw* A = reinterpret_cast<const bf16raw*>(p.A);
-  const bf16raw* W = reinterpret_cast<const bf16raw*>(p.W);
-  const int colbase = wid * 16 * NB + lg * NV;  // this lane's NV contiguous output channels
+  const bf16raw* W = reinterpret_cast<const bf16raw*>(p.W) + (size_t)sl * NS * p.ldw;
+  const int n0 = sl * NS;
+  const int colbase = n0 + wid * 16 * NB + lg * NV;  // this lane's NV contiguous output channels
+  const int wslot = sl * WV + wid;                    // partial-statistics column of this wave
 
   // ---- resident weight: fragment (nb, kb), MFMA row lr -> output channel
   v4u wf[NB][KB];
@@ -130,21 +180,25 @@ __global__ __launch_bounds__(64 * WV) void gemm_ws_kernel(GemmRows p) {
   const float oal = (OPK == OP_PRELU_NORM || N1B) ? p.aop.alpha[0] : 0.f;
   const bf16raw* H1 = reinterpret_cast<const bf16raw*>(p.aop.aux);
   bf16raw* GH = reinterpret_cast<bf16raw*>(p.aop.aout);
-  v4u rh[N1B ? NA : 1];   // N1B: h1 chunks beside the gradient chunks
+  v4u rh[PF][N1B ? NA : 1];   // N1B: h1 chunks beside the gradient chunks
+  v4u ghv[N1B ? NA : 1];      // N1B: dL/dh1 chunks of the staged tile, stored after the loads
   float calpha = 0.f;     // N1B: this thread's PReLU-1 alpha gradient over its valid rows
   // Loads are issued one tile ahead together with the statistics they need, so
   // that no wait inside an iteration has to drain the next tile's prefetch
   // (vmcnt retires loads in issue order).
-  v4u ra[NA];
-  float2 ast[NA];
-  auto load_a = [&](int t) __attribute__((always_inline)) {
+  // Ring of PF register tiles: tile t lives in slot (t - t0) % PF (static indices:
+  // the tile loop is unrolled by PF).
+  v4u ra[PF][NA];
+  float2 ast[PF][NA];
+  auto load_a = [&](int t, auto slot) __attribute__((always_inline)) {
+    constexpr int s = decltype(slot)::value;
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
       const int r = t * TM + rl0 + j * RSTEP;
-      if constexpr (CTN_WS_EXP & 2) ra[j] = v4u{(uint32_t)r, 0u, 0u, 0u};
-      else ra[j] = ldg16(A + (size_t)r * p.lda + kc * 8);
-      if constexpr (N1B) rh[j] = ldg16(H1 + (size_t)r * p.lda + kc * 8);
-      if constexpr (OPK != OP_PLAIN && !FOLDS) ast[j] = p.aop.stats[stat_index<NK>(r, Kp)];
+      if constexpr (CTN_WS_EXP & 2) ra[s][j] = v4u{(uint32_t)r, 0u, 0u, 0u};
+      else ra[s][j] = ldg16(A + (size_t)r * p.lda + kc * 8);
+      if constexpr (N1B) rh[s][j] = ldg16(H1 + (size_t)r * p.lda + kc * 8);
+      if constexpr (OPK != OP_PLAIN && !FOLDS) ast[s][j] = p.aop.stats[stat_index<NK>(r, Kp)];
     }
   };
   // ra -> LDS image of tile t (fragment (mb, kb) at (mb*KB + kb) KiB).  Rows of padded
@@ -152,13 +206,14 @@ __global__ __launch_bounds__(64 * WV) void gemm_ws_kernel(GemmRows p) {
   // (+ the residual's zero row) and contributes nothing to any statistic.
   // tu may run past the range: such tiles are clamped to the last one (staged again,
   // never stored, and not counted in the alpha gradient).
-  auto stage = [&](auto le1, int tu, char* buf) __attribute__((always_inline)) {
+  auto stage = [&](auto le1, int tu, char* buf, auto slot) __attribute__((always_inline)) {
     constexpr bool LE1 = decltype(le1)::value;
+    constexpr int s = decltype(slot)::value;
     const int t = tu < t1 ? tu : t1 - 1;
     const int tk = (t * TM) % Kp;   // frame index of the tile's first row (wave-uniform)
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
-      v4u v = ra[j];
+      v4u v = ra[s][j];
       const int r = rl0 + j * RSTEP;
       if constexpr (N1B) {
         // same arithmetic as norm1_bwd_kernel (ctn_tcn.hip), element by element
@@ -166,7 +221,7 @@ __global__ __launch_bounds__(64 * WV) void gemm_ws_kernel(GemmRows p) {
         const float2 sm = sst[m], st = sst1[m];
         float g[8], h[8];
         unpack_bf16x8(v, g);
-        unpack_bf16x8(rh[j], h);
+        unpack_bf16x8(rh[s][j], h);
         float ca = 0.f;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -183,7 +238,7 @@ __global__ __launch_bounds__(64 * WV) void gemm_ws_kernel(GemmRows p) {
         }
         calpha += (tu < t1 && tk + r < Kv) ? ca : 0.f;
       } else if constexpr (OPK != OP_PLAIN) {
-        const float2 st = FOLDS ? sst[(t * TM) / Kp] : ast[j];
+        const float2 st = FOLDS ? sst[(t * TM) / Kp] : ast[s][j];
         float f[8];
         unpack_bf16x8(v, f);
         const f32x2_t m2 = {st.x, st.x};
@@ -197,9 +252,17 @@ __global__ __launch_bounds__(64 * WV) void gemm_ws_kernel(GemmRows p) {
       }
       const v4u z = v4u{0u, 0u, 0u, 0u};
       v = tk + r < Kv ? v : z;   // tiles never straddle utterances (Kp % TM == 0)
-      if constexpr (N1B)         // dL/dh1 for the weight-gradient kernel (padded rows 0)
-        if (tu < t1) stg16(GH + (size_t)(t * TM + r) * p.lda + kc * 8, v);
+      if constexpr (N1B) ghv[j] = v;   // dL/dh1 for the weight-gradient kernel (padded rows 0)
       stg16(buf + (r >> 4) * KB * 1024 + ws_slot(r & 15, kc & 3, kc >> 2), v);
+    }
+  };
+  // global store of the dL/dh1 chunks staged by stage(tu)
+  auto store_gh = [&](int tu) __attribute__((always_inline)) {
+    if constexpr (N1B) {
+      if (tu < t1) {
+#pragma unroll
+        for (int j = 0; j < NA; ++j) stg16(GH + (size_t)(tu * TM + rl0 + j * RSTEP) * p.lda + kc * 8, ghv[j]);
+      }
     }
   };
 
@@ -208,7 +271,7 @@ __global__ __launch_bounds__(64 * WV) void gemm_ws_kernel(GemmRows p) {
   constexpr bool HAS_STATS = EPI == EPI_PRELU_STATS || EPI == EPI_NORM_BWD;
   const float eal = (EPI == EPI_PRELU_STATS || EPI == EPI_NORM_BWD) ? p.alpha[0] : 0.f;
   if constexpr (EPI == EPI_NORM_BWD)
-    for (int c = tid; c < NB * 16 * WV; c += NT) sgam[c] = p.gamma[c];
+    for (int c = tid; c < NS; c += NT) sgam[c] = p.gamma[n0 + c];
   const bf16raw* Rp = reinterpret_cast<const bf16raw*>(p.R);
   bf16raw* Cp = reinterpret_cast<bf16raw*>(p.C);
   v4u rn[MB][Q];   // epilogue operand of the current tile (loaded one tile ahead)
@@ -226,21 +289,44 @@ __global__ __launch_bounds__(64 * WV) void gemm_ws_kernel(GemmRows p) {
     }
   };
 
+  // LDS fragment reads run LA k-steps ahead of the MFMAs that consume them (a
+  // register window of LA+1 steps), so a k-step's MFMAs never wait on a read issued
+  // just before them (one read in flight per step exposed the LDS latency 16x/tile).
+  constexpr int LA = SWP ? 0 : WV == 16 ? CTN_WS_LA16 : CTN_WS_LA8;
   auto mfma_tile = [&](const char* buf, f32x4_t (&acc)[MB][NB]) __attribute__((always_inline)) {
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) acc[mb][nb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    v4u bw[LA + 1][MB];
+    auto rd = [&](int kb) __attribute__((always_inline)) {
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) bw[kb % (LA + 1)][mb] = ldg16(buf + mb * KB * 1024 + ws_slot(lr, lg, kb));
+    };
+#pragma unroll
+    for (int kb = 0; kb < LA && kb < KB; ++kb) rd(kb);
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) {
+      if (kb + LA < KB) rd(kb + LA);
 #pragma unroll
       for (int mb = 0; mb < MB; ++mb) {
-        const v4u b = ldg16(buf + mb * KB * 1024 + ws_slot(lr, lg, kb));
+        const v4u b = bw[kb % (LA + 1)][mb];
 #pragma unroll
         for (int nb = 0; nb < NB; ++nb)
           if constexpr (CTN_WS_EXP & 4) acc[mb][nb][kb & 3] += __uint_as_float(b[0] ^ wf[nb][kb][1]);
           else acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wf[nb][kb]),
                                                                      __builtin_bit_cast(bf16x8_t, b), acc[mb][nb], 0, 0, 0);
+      }
+    }
+    if constexpr (LA > 0 && !(CTN_WS_EXP & 4)) {
+      // pin the interleave (the register-pressure scheduler would otherwise pull each
+      // read down to its MFMAs): prologue reads, then per k-step its look-ahead reads
+      // followed by its MFMAs
+      __builtin_amdgcn_sched_group_barrier(0x100, MB * (LA < KB ? LA : KB), 0);
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+        if (kb + LA < KB) __builtin_amdgcn_sched_group_barrier(0x100, MB, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, MB * NB, 0);
       }
     }
   };
@@ -249,14 +335,28 @@ __global__ __launch_bounds__(64 * WV) void gemm_ws_kernel(GemmRows p) {
   double run_s = 0.0, run_q = 0.0;
   const int tpu = Kp / TM, m0 = t0 / tpu;
   int run_m = m0;
-  const int kmax = ws_runs_kmax(ntile, (int)gridDim.x, tpu);
+  const int kmax = ws_runs_kmax(ntile, nr, tpu);
+  // per-lane fp64 partials of the current utterance run, reduced over the wave and
+  // stored once per run
   auto flush_run = [&]() __attribute__((always_inline)) {
-    p.grp_slab[((size_t)blockIdx.x * WV + wid) * kmax + (run_m - m0)] = make_double2(run_s, run_q);
+    const double s = wave_sum(run_s), q = wave_sum(run_q);
+    if (lane == 0) p.grp_slab[((size_t)rr * (S * WV) + wslot) * kmax + (run_m - m0)] = make_double2(s, q);
   };
 
   // epilogue of tile t from its accumulators: lane holds rows t*TM + mb*16 + lr,
-  // channels colbase .. colbase+NV-1.  Branch-free (packed fp32 math).
-  auto epilogue = [&](auto le1, int t, const f32x4_t (&acc)[MB][NB]) __attribute__((always_inline)) {
+  // channels colbase .. colbase+NV-1.  Branch-free (packed fp32 math).  The math
+  // leaves the packed outputs in ov; store_out(t) writes them.
+  v4u ov[MB][Q];
+  auto store_out = [&](int t) __attribute__((always_inline)) {
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      bf16raw* dst = Cp + (size_t)(t * TM + mb * 16 + lr) * p.ldc + colbase;
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        if constexpr (!(CTN_WS_EXP & 1)) stg16(dst + q * 8, ov[mb][q]);
+    }
+  };
+  auto epilogue_math = [&](auto le1, int t, const f32x4_t (&acc)[MB][NB]) __attribute__((always_inline)) {
     constexpr bool LE1 = decltype(le1)::value;
     f32x2_t gs2 = {0.f, 0.f}, gq2 = {0.f, 0.f};   // gLN partials over the tile
 #pragma unroll
@@ -291,8 +391,8 @@ __global__ __launch_bounds__(64 * WV) void gemm_ws_kernel(GemmRows p) {
         for (int q = 0; q < Q; ++q) {
           float f[8];
           unpack_bf16x8(rn[mb][q], f);
-          const float4 g0 = *reinterpret_cast<const float4*>(&sgam[colbase + q * 8]);
-          const float4 g1 = *reinterpret_cast<const float4*>(&sgam[colbase + q * 8 + 4]);
+          const float4 g0 = *reinterpret_cast<const float4*>(&sgam[colbase - n0 + q * 8]);
+          const float4 g1 = *reinterpret_cast<const float4*>(&sgam[colbase - n0 + q * 8 + 4]);
           const f32x2_t gq[4] = {{g0.x, g0.y}, {g0.z, g0.w}, {g1.x, g1.y}, {g1.z, g1.w}};
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -303,15 +403,10 @@ __global__ __launch_bounds__(64 * WV) void gemm_ws_kernel(GemmRows p) {
           }
         }
       }
-      {
-        bf16raw* dst = Cp + (size_t)r * p.ldc + colbase;
 #pragma unroll
-        for (int q = 0; q < Q; ++q) {
-          const v4u o = {pk_bf16(v2[q * 4][0], v2[q * 4][1]), pk_bf16(v2[q * 4 + 1][0], v2[q * 4 + 1][1]),
-                         pk_bf16(v2[q * 4 + 2][0], v2[q * 4 + 2][1]), pk_bf16(v2[q * 4 + 3][0], v2[q * 4 + 3][1])};
-          if constexpr (!(CTN_WS_EXP & 1)) stg16(dst + q * 8, o);
-        }
-      }
+      for (int q = 0; q < Q; ++q)
+        ov[mb][q] = v4u{pk_bf16(v2[q * 4][0], v2[q * 4][1]), pk_bf16(v2[q * 4 + 1][0], v2[q * 4 + 1][1]),
+                        pk_bf16(v2[q * 4 + 2][0], v2[q * 4 + 2][1]), pk_bf16(v2[q * 4 + 3][0], v2[q * 4 + 3][1])};
       if constexpr (HAS_STATS) {
         if constexpr (NK == NORM_GLN) {
           if constexpr (MB == 1) {
@@ -327,22 +422,25 @@ __global__ __launch_bounds__(64 * WV) void gemm_ws_kernel(GemmRows p) {
           float s = s2[0] + s2[1], ss = q2[0] + q2[1];
           s += __shfl_xor(s, 16, 64); ss += __shfl_xor(ss, 16, 64);
           s += __shfl_xor(s, 32, 64); ss += __shfl_xor(ss, 32, 64);
-          p.grp_slab[(size_t)r * WV + wid] = make_double2((double)s, (double)ss);
+          p.grp_slab[(size_t)r * (S * WV) + wslot] = make_double2((double)s, (double)ss);
         }
       }
     }
     if constexpr (HAS_STATS && NK == NORM_GLN) {
       // the wave's tiles of one utterance accumulate into one run partial (WsRuns)
-      const float s = wave_sum_dpp(gs2[0] + gs2[1]), ss = wave_sum_dpp(gq2[0] + gq2[1]);
       const int m = (t * TM) / Kp;
       if (m != run_m) {
         flush_run();
         run_m = m;
         run_s = run_q = 0.0;
       }
-      run_s += (double)s;
-      run_q += (double)ss;
+      run_s += (double)(gs2[0] + gs2[1]);
+      run_q += (double)(gq2[0] + gq2[1]);
     }
+  };
+  auto epilogue = [&](auto le1, int t, const f32x4_t (&acc)[MB][NB]) __attribute__((always_inline)) {
+    epilogue_math(le1, t, acc);
+    store_out(t);
   };
 
 #pragma unroll
@@ -368,37 +466,56 @@ __global__ __launch_bounds__(64 * WV) void gemm_ws_kernel(GemmRows p) {
   auto run = [&](auto le1) __attribute__((always_inline)) {
     if constexpr (!SWP) {
       f32x4_t acc[MB][NB];
-      load_a(t0);
+      // prologue: tiles t0 .. t0+PF-1 into slots 0 .. PF-1; t0 staged; t0+PF into slot 0
+      static_for<PF>([&](auto i) { load_a(clampt(t0 + decltype(i)::value), i); });
       load_r(t0);
-      stage(le1, t0, sA[t0 & 1]);
-      load_a(clampt(t0 + 1));
-      for (int t = t0; t < t1; ++t) {
-        lds_barrier();
-        mfma_tile(sA[t & 1], acc);
-        __builtin_amdgcn_sched_barrier(0);
-        epilogue(le1, t, acc);
-        load_r(clampt(t + 1));
-        stage(le1, t + 1, sA[(t + 1) & 1]);
-        load_a(clampt(t + 2));
+      stage(le1, t0, sA[t0 & 1], std::integral_constant<int, 0>{});
+      store_gh(t0);
+      load_a(clampt(t0 + PF), std::integral_constant<int, 0>{});
+      for (int tb = t0; tb < t1; tb += PF) {
+        static_for<PF>([&](auto u) {
+          constexpr int nx = (decltype(u)::value + 1) % PF;   // slot of tile t+1
+          const int t = tb + decltype(u)::value;
+          if (PF == 1 || t < t1) {
+            lds_barrier();
+            mfma_tile(sA[t & 1], acc);
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (CTN_WS_ORDER == 1) {
+              // next tile's operand (its buffer's last reader finished before the barrier)
+              stage(le1, t + 1, sA[(t + 1) & 1], std::integral_constant<int, nx>{});
+              load_a(clampt(t + 1 + PF), std::integral_constant<int, nx>{});
+              epilogue_math(le1, t, acc);
+              load_r(clampt(t + 1));   // rn(t) consumed above
+              store_out(t);
+              store_gh(t + 1);
+            } else {
+              epilogue(le1, t, acc);
+              load_r(clampt(t + 1));
+              stage(le1, t + 1, sA[(t + 1) & 1], std::integral_constant<int, nx>{});
+              store_gh(t + 1);
+              load_a(clampt(t + 1 + PF), std::integral_constant<int, nx>{});
+            }
+          }
+        });
       }
     } else {
       f32x4_t accP[MB][NB], accC[MB][NB];
-      load_a(t0);
-      stage(le1, t0, sA[t0 & 1]);
-      load_a(clampt(t0 + 1));
+      load_a(t0, std::integral_constant<int, 0>{});
+      stage(le1, t0, sA[t0 & 1], std::integral_constant<int, 0>{});
+      load_a(clampt(t0 + 1), std::integral_constant<int, 0>{});
       lds_barrier();
       mfma_tile(sA[t0 & 1], accP);
       load_r(t0);
-      stage(le1, t0 + 1, sA[(t0 + 1) & 1]);
-      load_a(clampt(t0 + 2));
+      stage(le1, t0 + 1, sA[(t0 + 1) & 1], std::integral_constant<int, 0>{});
+      load_a(clampt(t0 + 2), std::integral_constant<int, 0>{});
       // unrolled by two so the two accumulator sets swap roles without copies
       auto step = [&](int t, f32x4_t (&cur)[MB][NB], f32x4_t (&prev)[MB][NB]) __attribute__((always_inline)) {
         lds_barrier();
         mfma_tile(sA[t & 1], cur);
         epilogue(le1, t - 1, prev);
         load_r(t);
-        stage(le1, t + 1, sA[(t + 1) & 1]);
-        load_a(clampt(t + 2));
+        stage(le1, t + 1, sA[(t + 1) & 1], std::integral_constant<int, 0>{});
+        load_a(clampt(t + 2), std::integral_constant<int, 0>{});
       };
       int t = t0 + 1;
       for (; t + 1 < t1; t += 2) {
@@ -475,22 +592,24 @@ bool gemm_ws_can_fold(DType dt, const GemmRows& p) {
   return gemm_ws_eligible(dt, p) && p.aop.kind != OP_PLAIN && p.aop.norm == NORM_GLN;
 }
 
-// frame rows per tile (16, or 32 for the 16-wave configuration)
+// frame rows per tile (16, or 32 for the wide configuration)
 static int ws_tile_rows(const GemmRows& p);
-static int ws_waves(const GemmRows& p);
+static int ws_waves(const GemmRows& p);     // waves per row range (all slices)
+static int ws_slices(const GemmRows& p);
 
-int gemm_ws_grid(const GemmRows& p) {
+static int ws_ranges(const GemmRows& p) {
   const long nt = p.g.rows() / ws_tile_rows(p);
   return (int)(nt < WS_GRID ? nt : WS_GRID);
 }
+int gemm_ws_grid(const GemmRows& p) { return ws_ranges(p) * ws_slices(p); }
 
-// gLN partials use the run layout (WsRuns): grid*waves*kmax entries in all,
+// gLN partials use the run layout (WsRuns): ranges*waves*kmax entries in all,
 // sized here as G groups of ceil(entries / G) parts; cLN: waves parts per row
 WsRuns gemm_ws_runs(const GemmRows& p) {
   WsRuns w;
   const int tm = ws_tile_rows(p);
   w.ntile = (int)(p.g.rows() / tm);
-  w.grid = gemm_ws_grid(p);
+  w.grid = ws_ranges(p);
   w.tpu = p.g.Kp / tm;
   w.waves = ws_waves(p);
   w.kmax = ws_runs_kmax(w.ntile, w.grid, w.tpu);
@@ -504,10 +623,18 @@ int gemm_ws_group_parts(const GemmRows& p) {
   return (int)((entries + p.g.M - 1) / p.g.M);
 }
 
-// Register-staged kernel configurations: (NB, KB, waves, m-blocks).  Nout = 512
-// runs 16 waves of 32 channels (64 weight VGPRs per lane: 4 waves per SIMD, so one
-// wave's latency hides behind another's work) on 32-row tiles; Nout = 256 runs
-// 8 waves of 32 channels with a 128-register weight slice on 16-row tiles.
+static bool ws_wide(const GemmRows& p) {   // Nout = 512 on 32-row tiles (16 waves per range)
+  return p.Nout == 512 && p.Kred == 256 && p.epi != EPI_NORM_BWD;
+}
+static int ws_waves(const GemmRows& p) { return ws_wide(p) ? 16 : 8; }
+static int ws_tile_rows(const GemmRows& p) { return ws_wide(p) ? 32 : WS_TM; }
+static int ws_slices(const GemmRows& p) { return ws_wide(p) ? CTN_WS_S512 : 1; }
+
+// Register-staged kernel configurations: (NB, KB, waves, m-blocks, slices).  Nout = 512
+// runs 16 waves of 32 channels per 32-row range (64 weight VGPRs per lane: 4 waves
+// per SIMD, so one wave's latency hides behind another's work), as one 16-wave
+// workgroup or as two 8-wave slice workgroups (CTN_WS_S512); Nout = 256 runs 8 waves
+// of 32 channels with a 128-register weight slice on 16-row tiles.
 template <int OPK, int NK, int EPI>
 static hipError_t ws_launch_shape(const GemmRows& p, hipStream_t s) {
   int nb = 0, kb = 0;
@@ -516,6 +643,8 @@ static hipError_t ws_launch_shape(const GemmRows& p, hipStream_t s) {
   if (nb == 4 && kb == 8) {
     if constexpr (EPI == EPI_NORM_BWD)   // its epilogue needs more than the 128 registers of 16 waves
       hipLaunchKernelGGL((gemm_ws_kernel<OPK, NK, EPI, 4, 8, 8, 1>), grid, dim3(512), 0, s, p);
+    else if (ws_slices(p) == 2)
+      hipLaunchKernelGGL((gemm_ws_kernel<OPK, NK, EPI, 2, 8, 8, 2, 2>), grid, dim3(512), 0, s, p);
     else
       hipLaunchKernelGGL((gemm_ws_kernel<OPK, NK, EPI, 2, 8, 16, 2>), grid, dim3(1024), 0, s, p);
   }
@@ -525,12 +654,6 @@ static hipError_t ws_launch_shape(const GemmRows& p, hipStream_t s) {
     hipLaunchKernelGGL((gemm_ws_kernel<OPK, NK, EPI, 2, 8, 8, 1>), grid, dim3(512), 0, s, p);
   return hipGetLastError();
 }
-
-static bool ws_wide(const GemmRows& p) {   // the 16-wave, 32-row configuration
-  return p.Nout == 512 && p.Kred == 256 && p.epi != EPI_NORM_BWD;
-}
-static int ws_waves(const GemmRows& p) { return ws_wide(p) ? 16 : 8; }
-static int ws_tile_rows(const GemmRows& p) { return ws_wide(p) ? 32 : WS_TM; }
 
 template <int NK>
 static hipError_t ws_launch_nk(const GemmRows& p, hipStream_t s) {
