@@ -50,6 +50,21 @@ def _mask_code(mask_nonlinear):
     raise ValueError("Unsupported mask non-linear function")      # conv_tasnet.py:207-208
 
 
+def _io_dtype(t):
+    return t.dtype if t.dtype in (torch.float32, torch.bfloat16) else torch.float32
+
+
+def _norm_rows(norm_mod, rows, fr):
+    """A block norm module applied to frame rows: gLN / cLN on the HIP path
+    (ctn_layernorm_*); nn.BatchNorm1d — chose_norm's fallback, a torch module in the
+    reference as well — on the NCW view of the rows."""
+    if isinstance(norm_mod, (GlobalLayerNorm, ChannelwiseLayerNorm)):
+        code = L.NORM_GLN if isinstance(norm_mod, GlobalLayerNorm) else L.NORM_CLN
+        return ops.LayerNormFn.apply(rows, fr, code, norm_mod.gamma, norm_mod.beta)
+    y = norm_mod(ops.rows_to_ncw(rows, fr, torch.float32))
+    return ops.ncw_to_rows(y, fr, rows.dtype)
+
+
 class ConvTasNet(nn.Module):
     def __init__(self, N, L, B, H, P, X, R, C, norm_type="gLN", causal=False,
                  mask_nonlinear='relu'):
@@ -200,10 +215,26 @@ class TemporalConvNet(nn.Module):
                 yield blk
 
     def forward(self, mixture_w):
-        """mixture_w [M, N, K] -> est_mask [M, C, N, K] (conv_tasnet.py:192-209)."""
-        raise L.CtnLibraryError(
-            "standalone TemporalConvNet.forward is not exposed by the HIP path yet; "
-            "call ConvTasNet.forward (fused encoder/separator/decoder)")
+        """mixture_w [M, N, K] -> est_mask [M, C, N, K] (conv_tasnet.py:192-209).
+
+        Stand-alone call: cLN, bottleneck, mask conv and nonlinearity as separate
+        native layers (ctn_layernorm / ctn_conv1x1 / ctn_mask), the blocks as in
+        ConvTasNet.forward (ctn_tblock).  Activations in fp32, or bf16 under
+        torch.autocast; the mask is returned in that dtype."""
+        L.require_device(mixture_w, "TemporalConvNet")
+        M, N, K = mixture_w.shape
+        fr = ops.Frames.of(M, K)
+        dt = _act_dtype(getattr(self, "act_dtype", None))
+        cln, bott, _, mask_conv = self.network
+        r = ops.ncw_to_rows(mixture_w, fr, dt)
+        r = ops.LayerNormFn.apply(r, fr, L.NORM_CLN, cln.gamma, cln.beta)
+        r = ops.Conv1x1Fn.apply(r, fr, bott.weight)
+        norm = _norm_code(self._norm_type)
+        for blk in self.blocks():
+            r = blk._forward_rows(r, fr, norm)
+        score = ops.Conv1x1Fn.apply(r, fr, mask_conv.weight)
+        mask = ops.MaskFn.apply(score, fr, self.C, _mask_code(self.mask_nonlinear))
+        return ops.rows_to_ncw(mask, fr).reshape(M, self.C, N, K)
 
 
 class TemporalBlock(nn.Module):
@@ -253,8 +284,9 @@ class TemporalBlock(nn.Module):
 
 
 class DepthwiseSeparableConv(nn.Module):
-    """conv_tasnet.py:241-272 — parameter container of the block's second half.
-    Its compute is fused into the TemporalBlock kernels (ctn_tblock_*)."""
+    """conv_tasnet.py:241-272.  Inside a TemporalBlock its compute is fused into the
+    block kernels (ctn_tblock_*); called on its own it runs the stand-alone layers
+    (ctn_depthwise / ctn_prelu / ctn_layernorm / ctn_conv1x1)."""
 
     def __init__(self, in_channels, out_channels, kernel_size,
                  stride, padding, dilation, norm_type="gLN", causal=False):
@@ -274,7 +306,23 @@ class DepthwiseSeparableConv(nn.Module):
             self.net = nn.Sequential(depthwise_conv, prelu, norm, pointwise_conv)
 
     def forward(self, x):
-        raise L.CtnLibraryError("DepthwiseSeparableConv runs fused inside TemporalBlock on the HIP path")
+        """x [M, C_in, K] -> [M, C_out, K] (conv_tasnet.py:265-272)."""
+        L.require_device(x, "DepthwiseSeparableConv")
+        M, C, K = x.shape
+        fr = ops.Frames.of(M, K)
+        causal = isinstance(self.net[1], Chomp1d)
+        dw = self.net[0]
+        P, dil = dw.kernel_size[0], dw.dilation[0]
+        if dw.stride[0] != 1 or dw.padding[0] != ((P - 1) * dil if causal else (P - 1) * dil // 2):
+            raise L.CtnLibraryError("DepthwiseSeparableConv: only the reference's stride 1 and padding "
+                                    "(conv_tasnet.py:177,188) are implemented")
+        prelu, norm, pw = self.net[2 if causal else 1], self.net[3 if causal else 2], self.net[-1]
+        r = ops.ncw_to_rows(x, fr, _io_dtype(x))
+        r = ops.DepthwiseFn.apply(r, fr, (P, dil, causal), dw.weight)
+        r = ops.PReLUFn.apply(r, fr, prelu.weight)
+        r = _norm_rows(norm, r, fr)
+        r = ops.Conv1x1Fn.apply(r, fr, pw.weight)
+        return ops.rows_to_ncw(r, fr)
 
 
 class Chomp1d(nn.Module):
@@ -300,8 +348,9 @@ def chose_norm(norm_type, channel_size):
 
 
 class ChannelwiseLayerNorm(nn.Module):
-    """Channel-wise Layer Normalization (cLN), conv_tasnet.py:307-329.
-    Applied inside the fused kernels (per-frame statistics, EPS=1e-8)."""
+    """Channel-wise Layer Normalization (cLN), conv_tasnet.py:307-329 (per-frame
+    statistics, biased variance, EPS=1e-8).  Fused into the encoder/block kernels
+    inside the model; on its own ctn_layernorm_* (CTN_NORM_CLN)."""
 
     def __init__(self, channel_size):
         super(ChannelwiseLayerNorm, self).__init__()
@@ -314,12 +363,22 @@ class ChannelwiseLayerNorm(nn.Module):
         self.beta.data.zero_()
 
     def forward(self, y):
-        raise L.CtnLibraryError("cLN runs fused inside the HIP kernels (EncoderFn / TBlockFn)")
+        """y [M, N, K] -> cLN(y) (conv_tasnet.py:319-329)."""
+        return _layer_norm_ncw(y, L.NORM_CLN, self.gamma, self.beta)
+
+
+def _layer_norm_ncw(y, code, gamma, beta):
+    L.require_device(y, "LayerNorm")
+    M, C, K = y.shape
+    fr = ops.Frames.of(M, K)
+    r = ops.LayerNormFn.apply(ops.ncw_to_rows(y, fr, _io_dtype(y)), fr, code, gamma, beta)
+    return ops.rows_to_ncw(r, fr)
 
 
 class GlobalLayerNorm(nn.Module):
-    """Global Layer Normalization (gLN), conv_tasnet.py:332-355.
-    Applied inside the fused kernels (per-utterance statistics, EPS=1e-8)."""
+    """Global Layer Normalization (gLN), conv_tasnet.py:332-355 (per-utterance
+    statistics over [N, K], EPS=1e-8).  Fused into the block kernels inside the
+    model; on its own ctn_layernorm_* (CTN_NORM_GLN)."""
 
     def __init__(self, channel_size):
         super(GlobalLayerNorm, self).__init__()
@@ -332,4 +391,5 @@ class GlobalLayerNorm(nn.Module):
         self.beta.data.zero_()
 
     def forward(self, y):
-        raise L.CtnLibraryError("gLN runs fused inside the HIP kernels (TBlockFn)")
+        """y [M, N, K] -> gLN(y) (conv_tasnet.py:344-355)."""
+        return _layer_norm_ncw(y, L.NORM_GLN, self.gamma, self.beta)

@@ -1166,3 +1166,268 @@ extern "C" int ctn_pack_weights(const ctn_weight_pack* packs, int n, void* strea
   }
   return CTN_OK;
 }
+
+// ===========================================================================
+// Stand-alone separator layers (ctn_layers.hip): the module forwards of
+// TemporalConvNet / DepthwiseSeparableConv / the layer norms when called on
+// their own, with their backward
+// ===========================================================================
+namespace {
+int rows_check(const ctn_rows_desc* d) {
+  if (!d) return fail(CTN_ERR_ARG, "null descriptor");
+  if (d->M <= 0 || d->K <= 0 || d->C <= 0) return fail(CTN_ERR_ARG, "M=%d K=%d C=%d", d->M, d->K, d->C);
+  if (d->Kp != ctn_padded_frames(d->K)) return fail(CTN_ERR_ARG, "Kp=%d != padded(K)", d->Kp);
+  if (d->dtype != CTN_DTYPE_F32 && d->dtype != CTN_DTYPE_BF16) return fail(CTN_ERR_ARG, "dtype %d", d->dtype);
+  if ((long)d->M * d->Kp * d->C >= (1L << 31)) return fail(CTN_ERR_UNSUPPORTED, "tensor too large");
+  return CTN_OK;
+}
+Rows rows_of(const ctn_rows_desc* d) { return Rows{d->M, d->K, d->Kp}; }
+DType dtype_of(const ctn_rows_desc* d) { return d->dtype == CTN_DTYPE_BF16 ? BF16 : F32; }
+
+struct LnLayout {
+  double2* slab; float2* sums; float* part;
+  size_t bytes;
+};
+LnLayout ln_layout(const ctn_rows_desc* d, int norm, int bwd, void* ws) {
+  Carver c(ws);
+  LnLayout L{};
+  const Rows g = rows_of(d);
+  const long G = norm == CTN_NORM_GLN ? d->M : g.rows();
+  if (norm == CTN_NORM_GLN) L.slab = c.take<double2>((size_t)d->M * layer_norm_groups_nb(g) * sizeof(double2));
+  if (bwd) {
+    L.sums = c.take<float2>((size_t)G * sizeof(float2));
+    L.part = c.take<float>((size_t)layer_blocks(g) * 2 * d->C * sizeof(float));
+  }
+  L.bytes = c.off + 256;
+  return L;
+}
+int norm_check(int norm) {
+  return norm == CTN_NORM_GLN || norm == CTN_NORM_CLN ? CTN_OK
+                                                      : fail(CTN_ERR_UNSUPPORTED, "layer norm type %d", norm);
+}
+}  // namespace
+
+extern "C" size_t ctn_layernorm_workspace_bytes(const ctn_rows_desc* d, int norm_type, int backward) {
+  if (rows_check(d) || norm_check(norm_type)) return 0;
+  return ln_layout(d, norm_type, backward, nullptr).bytes;
+}
+
+extern "C" int ctn_layernorm_forward(const ctn_rows_desc* d, int norm_type, const void* x, const float* gamma,
+                                     const float* beta, void* y, float* stats, void* ws, size_t ws_bytes,
+                                     void* stream) {
+  if (int rc = rows_check(d)) return rc;
+  if (int rc = norm_check(norm_type)) return rc;
+  if (!x || !gamma || !beta || !y || !stats) return fail(CTN_ERR_ARG, "null pointer");
+  const LnLayout L = ln_layout(d, norm_type, 0, ws);
+  if (ws_bytes < L.bytes || (!ws && L.slab)) return fail(CTN_ERR_WORKSPACE, "workspace %zu < %zu", ws_bytes, L.bytes);
+  LayerArgs a{};
+  a.g = rows_of(d); a.C = d->C; a.x = x; a.y = y;
+  a.norm = norm_type == CTN_NORM_GLN ? NORM_GLN : NORM_CLN; a.eps = (float)kEps;
+  a.gamma = gamma; a.beta = beta; a.stats = reinterpret_cast<float2*>(stats); a.slab = L.slab;
+  CTN_HIP(launch_layer(dtype_of(d), LAYER_NORM_FWD, a, (hipStream_t)stream));
+  return CTN_OK;
+}
+
+extern "C" int ctn_layernorm_backward(const ctn_rows_desc* d, int norm_type, const void* x, const float* gamma,
+                                      const float* stats, const void* gy, void* gx, float* ggamma, float* gbeta,
+                                      void* ws, size_t ws_bytes, void* stream) {
+  if (int rc = rows_check(d)) return rc;
+  if (int rc = norm_check(norm_type)) return rc;
+  if (!x || !gamma || !stats || !gy || !gx || !ggamma || !gbeta) return fail(CTN_ERR_ARG, "null pointer");
+  const LnLayout L = ln_layout(d, norm_type, 1, ws);
+  if (!ws || ws_bytes < L.bytes) return fail(CTN_ERR_WORKSPACE, "workspace %zu < %zu", ws_bytes, L.bytes);
+  LayerArgs a{};
+  a.g = rows_of(d); a.C = d->C; a.x = x; a.gy = gy; a.gx = gx;
+  a.norm = norm_type == CTN_NORM_GLN ? NORM_GLN : NORM_CLN;
+  a.gamma = gamma; a.stats = const_cast<float2*>(reinterpret_cast<const float2*>(stats));
+  a.sums = L.sums; a.slab = L.slab; a.part = L.part; a.ggamma = ggamma; a.gbeta = gbeta;
+  CTN_HIP(launch_layer(dtype_of(d), LAYER_NORM_BWD, a, (hipStream_t)stream));
+  return CTN_OK;
+}
+
+extern "C" size_t ctn_prelu_workspace_bytes(const ctn_rows_desc* d) {
+  if (rows_check(d)) return 0;
+  return (size_t)layer_blocks(rows_of(d)) * sizeof(float) + 256;
+}
+
+extern "C" int ctn_prelu_forward(const ctn_rows_desc* d, const void* x, const float* alpha, void* y, void* stream) {
+  if (int rc = rows_check(d)) return rc;
+  if (!x || !alpha || !y) return fail(CTN_ERR_ARG, "null pointer");
+  LayerArgs a{};
+  a.g = rows_of(d); a.C = d->C; a.x = x; a.y = y; a.alpha = alpha;
+  CTN_HIP(launch_layer(dtype_of(d), LAYER_PRELU_FWD, a, (hipStream_t)stream));
+  return CTN_OK;
+}
+
+extern "C" int ctn_prelu_backward(const ctn_rows_desc* d, const void* x, const float* alpha, const void* gy, void* gx,
+                                  float* galpha, void* ws, size_t ws_bytes, void* stream) {
+  if (int rc = rows_check(d)) return rc;
+  if (!x || !alpha || !gy || !gx || !galpha) return fail(CTN_ERR_ARG, "null pointer");
+  if (!ws || ws_bytes < ctn_prelu_workspace_bytes(d)) return fail(CTN_ERR_WORKSPACE, "workspace too small");
+  LayerArgs a{};
+  a.g = rows_of(d); a.C = d->C; a.x = x; a.gy = gy; a.gx = gx; a.alpha = alpha; a.galpha = galpha;
+  a.part = reinterpret_cast<float*>(ws);
+  CTN_HIP(launch_layer(dtype_of(d), LAYER_PRELU_BWD, a, (hipStream_t)stream));
+  return CTN_OK;
+}
+
+namespace {
+// reference padding (conv_tasnet.py:188): (P-1)*d both sides, the causal copy chomped on
+// the right (Chomp1d) -> left pad (P-1)*d; otherwise (P-1)*d//2 both sides, output length
+// K only when (P-1)*d is even
+int dw_check(const ctn_rows_desc* d, int P, int dil, int causal, int* pad) {
+  if (P < 1 || P > 64 || dil < 1) return fail(CTN_ERR_ARG, "P=%d dilation=%d", P, dil);
+  if (causal) {
+    *pad = (P - 1) * dil;
+  } else {
+    if (((P - 1) * dil) % 2) return fail(CTN_ERR_UNSUPPORTED, "non-causal (P-1)*dilation odd: output length != K");
+    *pad = (P - 1) * dil / 2;
+  }
+  return CTN_OK;
+}
+}  // namespace
+
+extern "C" size_t ctn_depthwise_workspace_bytes(const ctn_rows_desc* d, int P) {
+  if (rows_check(d) || P < 1) return 0;
+  return (size_t)layer_blocks(rows_of(d)) * d->C * P * sizeof(float) + 256;
+}
+
+extern "C" int ctn_depthwise_forward(const ctn_rows_desc* d, int P, int dilation, int causal, const void* x,
+                                     const float* w, void* y, void* stream) {
+  if (int rc = rows_check(d)) return rc;
+  int pad = 0;
+  if (int rc = dw_check(d, P, dilation, causal, &pad)) return rc;
+  if (!x || !w || !y) return fail(CTN_ERR_ARG, "null pointer");
+  LayerArgs a{};
+  a.g = rows_of(d); a.C = d->C; a.x = x; a.y = y; a.P = P; a.dil = dilation; a.pad = pad; a.w = w;
+  CTN_HIP(launch_layer(dtype_of(d), LAYER_DW_FWD, a, (hipStream_t)stream));
+  return CTN_OK;
+}
+
+extern "C" int ctn_depthwise_backward(const ctn_rows_desc* d, int P, int dilation, int causal, const void* x,
+                                      const float* w, const void* gy, void* gx, float* gw, void* ws, size_t ws_bytes,
+                                      void* stream) {
+  if (int rc = rows_check(d)) return rc;
+  int pad = 0;
+  if (int rc = dw_check(d, P, dilation, causal, &pad)) return rc;
+  if (!x || !w || !gy || !gx || !gw) return fail(CTN_ERR_ARG, "null pointer");
+  if (!ws || ws_bytes < ctn_depthwise_workspace_bytes(d, P)) return fail(CTN_ERR_WORKSPACE, "workspace too small");
+  LayerArgs a{};
+  a.g = rows_of(d); a.C = d->C; a.x = x; a.gy = gy; a.gx = gx; a.P = P; a.dil = dilation; a.pad = pad;
+  a.w = w; a.gw = gw; a.part = reinterpret_cast<float*>(ws);
+  CTN_HIP(launch_layer(dtype_of(d), LAYER_DW_BWD, a, (hipStream_t)stream));
+  return CTN_OK;
+}
+
+namespace {
+struct C1Layout {
+  void* ws_w; void* ws_wt; float* cpart;
+  int chunks;
+  size_t bytes;
+};
+GemmCols c1_cols(const ctn_rows_desc* d, int cout) {
+  GemmCols gc{};
+  gc.g = rows_of(d); gc.P = cout; gc.Q = d->C;
+  return gc;
+}
+C1Layout c1_layout(const ctn_rows_desc* d, int cout, int bwd, void* ws) {
+  Carver c(ws);
+  C1Layout L{};
+  const size_t es = esize(d->dtype);
+  if (!bwd) {
+    if (d->dtype == CTN_DTYPE_BF16) L.ws_w = c.take<void>((size_t)cout * d->C * es);
+  } else {
+    L.ws_wt = c.take<void>((size_t)cout * d->C * es);
+    L.chunks = gemm_cols_default_chunks(c1_cols(d, cout));
+    L.cpart = c.take<float>((size_t)L.chunks * cout * d->C * sizeof(float));
+  }
+  L.bytes = c.off + 256;
+  return L;
+}
+int c1_check(const ctn_rows_desc* d, int cout) {
+  if (cout <= 0 || cout % 8 || d->C % 8) return fail(CTN_ERR_UNSUPPORTED, "1x1 conv %d -> %d: channels must be multiples of 8", d->C, cout);
+  return CTN_OK;
+}
+}  // namespace
+
+extern "C" size_t ctn_conv1x1_workspace_bytes(const ctn_rows_desc* d, int cout, int backward) {
+  if (rows_check(d) || c1_check(d, cout)) return 0;
+  return c1_layout(d, cout, backward, nullptr).bytes;
+}
+
+extern "C" int ctn_conv1x1_forward(const ctn_rows_desc* d, int cout, const void* x, const float* w, void* y, void* ws,
+                                   size_t ws_bytes, void* stream) {
+  if (int rc = rows_check(d)) return rc;
+  if (int rc = c1_check(d, cout)) return rc;
+  if (!x || !w || !y) return fail(CTN_ERR_ARG, "null pointer");
+  const C1Layout L = c1_layout(d, cout, 0, ws);
+  if (ws_bytes < L.bytes || (!ws && L.ws_w)) return fail(CTN_ERR_WORKSPACE, "workspace %zu < %zu", ws_bytes, L.bytes);
+  hipStream_t s = (hipStream_t)stream;
+  const DType dt = dtype_of(d);
+  const void* wst = w;
+  if (dt == BF16) {
+    CTN_HIP(launch_prep_weight(dt, w, cout, d->C, L.ws_w, nullptr, s));
+    wst = L.ws_w;
+  }
+  GemmRows g{};
+  g.g = rows_of(d); g.Kred = d->C; g.Nout = cout;
+  g.A = x; g.lda = d->C; g.W = wst; g.ldw = d->C;
+  g.epi = EPI_STORE; g.C = y; g.ldc = cout;
+  CTN_HIP(launch_gemm_rows(dt, g, s));
+  return CTN_OK;
+}
+
+extern "C" int ctn_conv1x1_backward(const ctn_rows_desc* d, int cout, const void* x, const float* w, const void* gy,
+                                    void* gx, float* gw, void* ws, size_t ws_bytes, void* stream) {
+  if (int rc = rows_check(d)) return rc;
+  if (int rc = c1_check(d, cout)) return rc;
+  if (!x || !w || !gy || !gx || !gw) return fail(CTN_ERR_ARG, "null pointer");
+  const C1Layout L = c1_layout(d, cout, 1, ws);
+  if (!ws || ws_bytes < L.bytes) return fail(CTN_ERR_WORKSPACE, "workspace %zu < %zu", ws_bytes, L.bytes);
+  hipStream_t s = (hipStream_t)stream;
+  const DType dt = dtype_of(d);
+  CTN_HIP(launch_prep_weight(dt, w, cout, d->C, nullptr, L.ws_wt, s));   // [C][cout]
+  GemmRows g{};
+  g.g = rows_of(d); g.Kred = cout; g.Nout = d->C;
+  g.A = gy; g.lda = cout; g.W = L.ws_wt; g.ldw = cout;
+  g.epi = EPI_STORE; g.C = gx; g.ldc = d->C;
+  CTN_HIP(launch_gemm_rows(dt, g, s));
+  GemmCols gc = c1_cols(d, cout);
+  gc.A = gy; gc.lda = cout; gc.B = x; gc.ldb = d->C;
+  gc.Cpart = L.cpart; gc.nchunks = L.chunks;
+  CTN_HIP(launch_gemm_cols(dt, gc, s));
+  SlabBatch sb{};
+  sb.d[sb.nd++] = SlabDesc{L.cpart, gw, L.chunks, cout * d->C, cout * d->C};
+  CTN_HIP(launch_slab_reduce(sb, nullptr, s));
+  return CTN_OK;
+}
+
+namespace {
+int mask_check(const ctn_rows_desc* d, int nspk, int mask_type) {
+  if (nspk < 1 || d->C % nspk) return fail(CTN_ERR_ARG, "C=%d not a multiple of nspk=%d", d->C, nspk);
+  if (mask_type != CTN_MASK_RELU && mask_type != CTN_MASK_SOFTMAX) return fail(CTN_ERR_ARG, "mask type %d", mask_type);
+  return CTN_OK;
+}
+}  // namespace
+
+extern "C" int ctn_mask_forward(const ctn_rows_desc* d, int nspk, int mask_type, const void* score, void* mask,
+                                void* stream) {
+  if (int rc = rows_check(d)) return rc;
+  if (int rc = mask_check(d, nspk, mask_type)) return rc;
+  if (!score || !mask) return fail(CTN_ERR_ARG, "null pointer");
+  LayerArgs a{};
+  a.g = rows_of(d); a.C = d->C; a.x = score; a.y = mask; a.S = nspk; a.mask_type = mask_type;
+  CTN_HIP(launch_layer(dtype_of(d), LAYER_MASK_FWD, a, (hipStream_t)stream));
+  return CTN_OK;
+}
+
+extern "C" int ctn_mask_backward(const ctn_rows_desc* d, int nspk, int mask_type, const void* score, const void* gmask,
+                                 void* gscore, void* stream) {
+  if (int rc = rows_check(d)) return rc;
+  if (int rc = mask_check(d, nspk, mask_type)) return rc;
+  if (!score || !gmask || !gscore) return fail(CTN_ERR_ARG, "null pointer");
+  LayerArgs a{};
+  a.g = rows_of(d); a.C = d->C; a.x = score; a.gy = gmask; a.gx = gscore; a.S = nspk; a.mask_type = mask_type;
+  CTN_HIP(launch_layer(dtype_of(d), LAYER_MASK_BWD, a, (hipStream_t)stream));
+  return CTN_OK;
+}

@@ -184,6 +184,37 @@ hipError_t launch_dw_fwd(DType dt, const DwArgs& a, hipStream_t s);
 hipError_t launch_dw_bwd(DType dt, const DwArgs& a, hipStream_t s);
 hipError_t launch_norm1_bwd(DType dt, const DwArgs& a, hipStream_t s);
 
+// ---- stand-alone separator layers on frame rows (ctn_layers.hip) ------------
+enum LayerOp {
+  LAYER_NORM_FWD, LAYER_NORM_BWD, LAYER_PRELU_FWD, LAYER_PRELU_BWD,
+  LAYER_DW_FWD, LAYER_DW_BWD, LAYER_MASK_FWD, LAYER_MASK_BWD
+};
+struct LayerArgs {
+  Rows g;
+  int C;                        // channels of x (mask: S*N)
+  const void* x; void* y;       // forward input / output (mask backward: x = score)
+  const void* gy; void* gx;     // backward
+  // norms
+  int norm = 0; float eps = 0.f;
+  const float* gamma = nullptr; const float* beta = nullptr;
+  float2* stats = nullptr;      // (mean, rstd): [M] gLN, [M*Kp] cLN (forward out, backward in)
+  float2* sums = nullptr;       // backward scratch: (mean g*gamma, mean g*gamma*xhat) per group
+  double2* slab = nullptr;      // gLN scratch [M * layer_norm_groups_nb]
+  float* ggamma = nullptr; float* gbeta = nullptr;
+  // PReLU
+  const float* alpha = nullptr; float* galpha = nullptr;
+  // depthwise
+  int P = 0, dil = 1, pad = 0;
+  const float* w = nullptr; float* gw = nullptr;
+  // mask
+  int S = 1, mask_type = 0;
+  // column / alpha partials [layer_blocks][...] and the slab-reduce scratch
+  float* part = nullptr; float* tmp = nullptr;
+};
+int layer_blocks(const Rows& g);            // row blocks of the partial reductions
+int layer_norm_groups_nb(const Rows& g);    // gLN partials per utterance
+hipError_t launch_layer(DType dt, LayerOp op, const LayerArgs& a, hipStream_t s);
+
 // ---- BatchNorm1d column statistics (ctn_bn.hip) -----------------------------
 struct BnArgs {
   Rows g;

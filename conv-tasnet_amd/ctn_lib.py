@@ -14,7 +14,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CTN_HIP_LIB", os.path.join(_HERE, "libctn_hip.so"))
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 DTYPE_F32, DTYPE_BF16 = 0, 1
 NORM_GLN, NORM_CLN, NORM_BN = 0, 1, 2
@@ -69,6 +69,10 @@ class PitDesc(ctypes.Structure):
 MASK_IDENTITY = 2
 
 
+class RowsDesc(ctypes.Structure):
+    _fields_ = [(n, c_int32) for n in ("M", "K", "Kp", "C", "dtype")]
+
+
 class OptSegment(ctypes.Structure):
     _fields_ = [("param", c_void_p), ("grad", c_void_p), ("exp_avg", c_void_p), ("exp_avg_sq", c_void_p),
                 ("numel", ctypes.c_int64)]
@@ -111,6 +115,25 @@ _SIGS = {
     "ctn_grad_clip_norm": (ctypes.c_int, [c_void_p, c_void_p, ctypes.c_int, ctypes.c_float, c_void_p, c_void_p,
                                           c_void_p]),
     "ctn_adam_step": (ctypes.c_int, [c_void_p, c_void_p, ctypes.c_int, c_void_p, c_void_p]),
+    "ctn_layernorm_workspace_bytes": (c_size_t, [c_void_p, ctypes.c_int, ctypes.c_int]),
+    "ctn_layernorm_forward": (ctypes.c_int, [c_void_p, ctypes.c_int] + [c_void_p] * 5 + [c_void_p, c_size_t,
+                                                                                       c_void_p]),
+    "ctn_layernorm_backward": (ctypes.c_int, [c_void_p, ctypes.c_int] + [c_void_p] * 7 + [c_void_p, c_size_t,
+                                                                                        c_void_p]),
+    "ctn_prelu_workspace_bytes": (c_size_t, [c_void_p]),
+    "ctn_prelu_forward": (ctypes.c_int, [c_void_p] * 5),
+    "ctn_prelu_backward": (ctypes.c_int, [c_void_p] * 6 + [c_void_p, c_size_t, c_void_p]),
+    "ctn_depthwise_workspace_bytes": (c_size_t, [c_void_p, ctypes.c_int]),
+    "ctn_depthwise_forward": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int] + [c_void_p] * 4),
+    "ctn_depthwise_backward": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int] + [c_void_p] * 5 +
+                               [c_void_p, c_size_t, c_void_p]),
+    "ctn_conv1x1_workspace_bytes": (c_size_t, [c_void_p, ctypes.c_int, ctypes.c_int]),
+    "ctn_conv1x1_forward": (ctypes.c_int, [c_void_p, ctypes.c_int] + [c_void_p] * 3 + [c_void_p, c_size_t, c_void_p]),
+    "ctn_conv1x1_backward": (ctypes.c_int, [c_void_p, ctypes.c_int] + [c_void_p] * 5 + [c_void_p, c_size_t,
+                                                                                      c_void_p]),
+    "ctn_mask_forward": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p]),
+    "ctn_mask_backward": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p,
+                                         c_void_p]),
     "ctn_timer_enable": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "ctn_timer_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
 }

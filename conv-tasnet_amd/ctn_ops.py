@@ -338,6 +338,9 @@ class PITFn(torch.autograd.Function):
                                     ws.data_ptr(), nb, L.stream_handle(dev)), "ctn_pit_forward")
         ctx.mark_dirty(est)
         ctx.mark_non_differentiable(best)
+        # outputs the caller does not differentiate (max_snr, the masked estimate) arrive
+        # in backward as None instead of zero-filled tensors
+        ctx.set_materialize_grads(False)
         ctx.save_for_backward(source, est, lengths, coef)
         return loss, max_snr, est, best
 
@@ -354,7 +357,189 @@ class PITFn(torch.autograd.Function):
         L.check(lib.ctn_pit_backward(ctypes.byref(desc), source.data_ptr(), est.data_ptr(), lengths.data_ptr(),
                                      coef.data_ptr(), gl.data_ptr(), L.ptr(gm), g_est.data_ptr(),
                                      L.stream_handle(dev)), "ctn_pit_backward")
-        if g_est_out is not None:
+        if g_est_out is not None:   # the in-place mask's gradient: zero beyond each length
             mask = (torch.arange(T, device=dev).unsqueeze(0) < lengths.unsqueeze(1)).unsqueeze(1)
-            g_est = g_est + g_est_out * mask
+            g_est.addcmul_(g_est_out, mask)
         return None, g_est, None
+
+
+# ----------------------------------------------------------------------------
+# stand-alone separator layers on frame rows (ctn_layers.hip; include/ctn.h ABI v4):
+# the module forwards of TemporalConvNet / DepthwiseSeparableConv / gLN / cLN when
+# they are called on their own (conv_tasnet.py:192-209, 265-272, 319-329, 344-355)
+# ----------------------------------------------------------------------------
+def rows_desc(fr: Frames, C: int, dtype) -> "L.RowsDesc":
+    return L.RowsDesc(fr.M, fr.K, fr.Kp, C, L.dtype_code(dtype))
+
+
+class LayerNormFn(torch.autograd.Function):
+    """rows [M*Kp, C] -> gLN / cLN rows (norm: L.NORM_GLN / L.NORM_CLN)."""
+
+    @staticmethod
+    def forward(ctx, x, fr: Frames, norm: int, gamma, beta):
+        lib = L.load()
+        L.require_device(x, "LayerNorm")
+        x = x.contiguous()
+        C = x.shape[1]
+        g, b = _f32(gamma), _f32(beta)
+        d = rows_desc(fr, C, x.dtype)
+        y = torch.empty_like(x)
+        G = fr.M if norm == L.NORM_GLN else fr.rows
+        stats = torch.empty(G, 2, dtype=torch.float32, device=x.device)
+        nb = lib.ctn_layernorm_workspace_bytes(ctypes.byref(d), norm, 0)
+        ws = L.workspace(nb, x.device)
+        L.check(lib.ctn_layernorm_forward(ctypes.byref(d), norm, x.data_ptr(), g.data_ptr(), b.data_ptr(),
+                                          y.data_ptr(), stats.data_ptr(), ws.data_ptr(), nb,
+                                          L.stream_handle(x.device)), "ctn_layernorm_forward")
+        ctx.fr, ctx.norm = fr, norm
+        ctx.save_for_backward(x, g, stats)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        lib = L.load()
+        x, g, stats = ctx.saved_tensors
+        gy = gy.to(x.dtype).contiguous()
+        d = rows_desc(ctx.fr, x.shape[1], x.dtype)
+        gx = torch.empty_like(x)
+        gg = torch.empty_like(g)
+        gb = torch.empty_like(g)
+        nb = lib.ctn_layernorm_workspace_bytes(ctypes.byref(d), ctx.norm, 1)
+        ws = L.workspace(nb, x.device)
+        L.check(lib.ctn_layernorm_backward(ctypes.byref(d), ctx.norm, x.data_ptr(), g.data_ptr(), stats.data_ptr(),
+                                           gy.data_ptr(), gx.data_ptr(), gg.data_ptr(), gb.data_ptr(),
+                                           ws.data_ptr(), nb, L.stream_handle(x.device)), "ctn_layernorm_backward")
+        return gx, None, None, gg, gb
+
+
+class PReLUFn(torch.autograd.Function):
+    """rows -> nn.PReLU() rows (one shared alpha)."""
+
+    @staticmethod
+    def forward(ctx, x, fr: Frames, alpha):
+        lib = L.load()
+        L.require_device(x, "PReLU")
+        x = x.contiguous()
+        a = _f32(alpha)
+        d = rows_desc(fr, x.shape[1], x.dtype)
+        y = torch.empty_like(x)
+        L.check(lib.ctn_prelu_forward(ctypes.byref(d), x.data_ptr(), a.data_ptr(), y.data_ptr(),
+                                      L.stream_handle(x.device)), "ctn_prelu_forward")
+        ctx.fr = fr
+        ctx.save_for_backward(x, a)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        lib = L.load()
+        x, a = ctx.saved_tensors
+        gy = gy.to(x.dtype).contiguous()
+        d = rows_desc(ctx.fr, x.shape[1], x.dtype)
+        gx = torch.empty_like(x)
+        ga = torch.empty_like(a)
+        nb = lib.ctn_prelu_workspace_bytes(ctypes.byref(d))
+        ws = L.workspace(nb, x.device)
+        L.check(lib.ctn_prelu_backward(ctypes.byref(d), x.data_ptr(), a.data_ptr(), gy.data_ptr(), gx.data_ptr(),
+                                       ga.data_ptr(), ws.data_ptr(), nb, L.stream_handle(x.device)),
+                "ctn_prelu_backward")
+        return gx, None, ga
+
+
+class DepthwiseFn(torch.autograd.Function):
+    """rows -> depthwise dilated conv rows (reference padding; causal = + Chomp1d)."""
+
+    @staticmethod
+    def forward(ctx, x, fr: Frames, geo: tuple, w):
+        P, dil, causal = geo
+        lib = L.load()
+        L.require_device(x, "DepthwiseConv")
+        x = x.contiguous()
+        wf = _f32(w)
+        d = rows_desc(fr, x.shape[1], x.dtype)
+        y = torch.empty_like(x)
+        L.check(lib.ctn_depthwise_forward(ctypes.byref(d), P, dil, int(causal), x.data_ptr(), wf.data_ptr(),
+                                          y.data_ptr(), L.stream_handle(x.device)), "ctn_depthwise_forward")
+        ctx.fr, ctx.geo = fr, geo
+        ctx.save_for_backward(x, wf)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        lib = L.load()
+        x, wf = ctx.saved_tensors
+        P, dil, causal = ctx.geo
+        gy = gy.to(x.dtype).contiguous()
+        d = rows_desc(ctx.fr, x.shape[1], x.dtype)
+        gx = torch.empty_like(x)
+        gw = torch.empty_like(wf)
+        nb = lib.ctn_depthwise_workspace_bytes(ctypes.byref(d), P)
+        ws = L.workspace(nb, x.device)
+        L.check(lib.ctn_depthwise_backward(ctypes.byref(d), P, dil, int(causal), x.data_ptr(), wf.data_ptr(),
+                                           gy.data_ptr(), gx.data_ptr(), gw.data_ptr(), ws.data_ptr(), nb,
+                                           L.stream_handle(x.device)), "ctn_depthwise_backward")
+        return gx, None, None, gw
+
+
+class Conv1x1Fn(torch.autograd.Function):
+    """rows [.., C] -> rows [.., cout] of a bias-free 1x1 conv (weight [cout, C, 1])."""
+
+    @staticmethod
+    def forward(ctx, x, fr: Frames, w):
+        lib = L.load()
+        L.require_device(x, "Conv1x1")
+        x = x.contiguous()
+        wf = _f32(w)
+        cout, C = wf.shape[0], x.shape[1]
+        d = rows_desc(fr, C, x.dtype)
+        y = x.new_empty(fr.rows, cout)
+        nb = lib.ctn_conv1x1_workspace_bytes(ctypes.byref(d), cout, 0)
+        ws = L.workspace(nb, x.device)
+        L.check(lib.ctn_conv1x1_forward(ctypes.byref(d), cout, x.data_ptr(), wf.data_ptr(), y.data_ptr(),
+                                        ws.data_ptr(), nb, L.stream_handle(x.device)), "ctn_conv1x1_forward")
+        ctx.fr = fr
+        ctx.save_for_backward(x, wf)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        lib = L.load()
+        x, wf = ctx.saved_tensors
+        cout, C = wf.shape[0], x.shape[1]
+        gy = gy.to(x.dtype).contiguous()
+        d = rows_desc(ctx.fr, C, x.dtype)
+        gx = torch.empty_like(x)
+        gw = torch.empty_like(wf)
+        nb = lib.ctn_conv1x1_workspace_bytes(ctypes.byref(d), cout, 1)
+        ws = L.workspace(nb, x.device)
+        L.check(lib.ctn_conv1x1_backward(ctypes.byref(d), cout, x.data_ptr(), wf.data_ptr(), gy.data_ptr(),
+                                         gx.data_ptr(), gw.data_ptr(), ws.data_ptr(), nb,
+                                         L.stream_handle(x.device)), "ctn_conv1x1_backward")
+        return gx, None, gw
+
+
+class MaskFn(torch.autograd.Function):
+    """score rows [.., S*N] -> mask rows (ReLU, or softmax over the S speakers)."""
+
+    @staticmethod
+    def forward(ctx, score, fr: Frames, nspk: int, mask_type: int):
+        lib = L.load()
+        L.require_device(score, "mask")
+        score = score.contiguous()
+        d = rows_desc(fr, score.shape[1], score.dtype)
+        mask = torch.empty_like(score)
+        L.check(lib.ctn_mask_forward(ctypes.byref(d), nspk, mask_type, score.data_ptr(), mask.data_ptr(),
+                                     L.stream_handle(score.device)), "ctn_mask_forward")
+        ctx.fr, ctx.nspk, ctx.mask_type = fr, nspk, mask_type
+        ctx.save_for_backward(score)
+        return mask
+
+    @staticmethod
+    def backward(ctx, gm):
+        lib = L.load()
+        (score,) = ctx.saved_tensors
+        gm = gm.to(score.dtype).contiguous()
+        d = rows_desc(ctx.fr, score.shape[1], score.dtype)
+        gs = torch.empty_like(score)
+        L.check(lib.ctn_mask_backward(ctypes.byref(d), ctx.nspk, ctx.mask_type, score.data_ptr(), gm.data_ptr(),
+                                      gs.data_ptr(), L.stream_handle(score.device)), "ctn_mask_backward")
+        return gs, None, None, None

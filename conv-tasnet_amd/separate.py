@@ -1,14 +1,19 @@
 #!/usr/bin/env python
 """Drop-in for ``src/separate.py``: separate every
-mixture of a directory or manifest and write PCM_16 wavs
-(``<name>.wav`` = the mixture, ``<name>_s<c>.wav`` = estimate c).
+mixture of a directory or manifest and write PCM_16 wavs.
 
-Same flags and output names as the reference, including its
-``os.path.basename(f).strip('.wav')`` naming (strip removes any of the
-characters ``.wav`` from both ends of the name).
-The forward runs on the HIP path (a ROCm device is required; the reference
-forces CUDA too, separate.py:44-46,64-66); wavs are written by audio_io
-(soundfile is not installed).
+For each input ``<dir>/<name>.wav`` the output directory receives
+``<stem>.wav`` (the mixture, trimmed to its length) and ``<stem>_s<c>.wav``
+(estimate c, 1-based).  ``<stem>`` reproduces the reference's
+``os.path.basename(f).strip('.wav')``: str.strip removes any of the characters
+``.``, ``w``, ``a``, ``v`` from BOTH ends, so ``"wave.wav"`` becomes ``"e"``
+ — kept so existing scoring scripts find the
+same files.  Same command-line flags as the reference.
+
+The forward is the HIP path (``ConvTasNet`` on a ROCm device; the reference
+also requires a GPU, separate.py:44-46,64-66), in inference mode; wavs are
+written by audio_io (soundfile is not installed).  For frame-by-frame causal
+models see ``streaming.StreamingSeparator``.
 """
 import argparse
 import os
@@ -37,38 +42,49 @@ parser.add_argument('--batch_size', default=1, type=int,
                     help='Batch size')
 
 
+def output_stem(path: str) -> str:
+    """Base name of the output files for mixture ``path`` (reference naming)."""
+    return os.path.basename(path).strip('.wav')
+
+
+class Separator:
+    """A loaded model on the device plus the writer for its estimates."""
+
+    def __init__(self, model_path: str, sample_rate: int, device=None):
+        self.model = ConvTasNet.load_model(model_path)
+        print(self.model)
+        self.device = torch.device(device or "cuda")
+        self.model.eval().to(self.device)
+        self.sample_rate = sample_rate
+
+    @torch.no_grad()
+    def estimate(self, mixture: torch.Tensor, lengths: torch.Tensor):
+        """Padded mixtures [B, T] -> (trimmed mixtures, trimmed estimates [C, T_b]) per utterance."""
+        mixture, lengths = mixture.to(self.device), lengths.to(self.device)
+        est = self.model(mixture)
+        return remove_pad(mixture, lengths), remove_pad(est, lengths)
+
+    def save(self, out_dir: str, name: str, mixture, estimates):
+        stem = os.path.join(out_dir, output_stem(name))
+        write_wav(stem + '.wav', mixture, self.sample_rate)
+        for c, est in enumerate(estimates, start=1):
+            write_wav('%s_s%d.wav' % (stem, c), est, self.sample_rate)
+
+    def run(self, loader, out_dir: str):
+        os.makedirs(out_dir, exist_ok=True)
+        for mixture, lengths, names in loader:
+            mixes, ests = self.estimate(mixture, lengths)
+            for name, mix, est in zip(names, mixes, ests):
+                self.save(out_dir, name, mix, est)
+
+
 def separate(args):
     if args.mix_dir is None and args.mix_json is None:
         print("Must provide mix_dir or mix_json! When providing mix_dir, "
               "mix_json is ignored.")
-
-    model = ConvTasNet.load_model(args.model_path)
-    print(model)
-    model.eval()
-    model.cuda()
-
-    eval_dataset = EvalDataset(args.mix_dir, args.mix_json,
-                               batch_size=args.batch_size,
-                               sample_rate=args.sample_rate)
-    eval_loader = EvalDataLoader(eval_dataset, batch_size=1)
-    os.makedirs(args.out_dir, exist_ok=True)
-
-    def write(inputs, filename, sr=args.sample_rate):
-        write_wav(filename, inputs, sr)
-
-    with torch.no_grad():
-        for (i, data) in enumerate(eval_loader):
-            mixture, mix_lengths, filenames = data
-            mixture, mix_lengths = mixture.cuda(), mix_lengths.cuda()
-            estimate_source = model(mixture)  # [B, C, T]
-            flat_estimate = remove_pad(estimate_source, mix_lengths)
-            mixture = remove_pad(mixture, mix_lengths)
-            for b, filename in enumerate(filenames):
-                filename = os.path.join(args.out_dir, os.path.basename(filename).strip('.wav'))
-                write(mixture[b], filename + '.wav')
-                C = flat_estimate[b].shape[0]
-                for c in range(C):
-                    write(flat_estimate[b][c], filename + '_s{}.wav'.format(c + 1))
+    sep = Separator(args.model_path, args.sample_rate)
+    dataset = EvalDataset(args.mix_dir, args.mix_json, batch_size=args.batch_size, sample_rate=args.sample_rate)
+    sep.run(EvalDataLoader(dataset, batch_size=1), args.out_dir)
 
 
 if __name__ == '__main__':

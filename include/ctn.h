@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define CTN_ABI_VERSION 3
+#define CTN_ABI_VERSION 4
 
 typedef enum { CTN_DTYPE_F32 = 0, CTN_DTYPE_BF16 = 1 } ctn_dtype;
 /* CTN_NORM_BN: torch.nn.BatchNorm1d, chose_norm's fallback branch (conv_tasnet.py:302-303) */
@@ -206,6 +206,59 @@ int ctn_grad_clip_norm(const ctn_opt_segment* segs, const ctn_opt_chunk* chunks,
 /* one Adam step of every segment (param, exp_avg, exp_avg_sq updated in place) */
 int ctn_adam_step(const ctn_opt_segment* segs, const ctn_opt_chunk* chunks, int nchunks, const ctn_adam_hparams* hp,
                   void* stream);
+
+/* -------------------------------------------------------------------------
+ * Stand-alone separator layers on frame rows [M*Kp][C] (ABI v4): what the fused
+ * calls above run inside themselves, exposed for the reference's module
+ * forwards called on their own — TemporalConvNet.forward (src/conv_tasnet.py:
+ * 192-209), DepthwiseSeparableConv.forward (:265-272), ChannelwiseLayerNorm.
+ * forward (:319-329), GlobalLayerNorm.forward (:344-355) — each with its
+ * backward.  Gradients are written, not accumulated.
+ * ------------------------------------------------------------------------- */
+typedef struct {
+  int32_t M, K, Kp;         /* utterances, frames, padded frames */
+  int32_t C;                /* channels of the input rows */
+  int32_t dtype;            /* ctn_dtype of activations */
+} ctn_rows_desc;
+
+/* gLN / cLN (norm_type CTN_NORM_GLN / CTN_NORM_CLN; EPS 1e-8 inside the sqrt,
+ * biased variance, conv_tasnet.py:10,327,353); gamma/beta [1,C,1]; stats
+ * [G][2] (mean, rstd), G = M (gLN) or M*Kp (cLN), written by forward */
+size_t ctn_layernorm_workspace_bytes(const ctn_rows_desc* d, int norm_type, int backward);
+int ctn_layernorm_forward(const ctn_rows_desc* d, int norm_type, const void* x, const float* gamma,
+                          const float* beta, void* y, float* stats, void* ws, size_t ws_bytes, void* stream);
+int ctn_layernorm_backward(const ctn_rows_desc* d, int norm_type, const void* x, const float* gamma,
+                           const float* stats, const void* gy, void* gx, float* ggamma, float* gbeta, void* ws,
+                           size_t ws_bytes, void* stream);
+
+/* nn.PReLU() with one shared alpha (conv_tasnet.py:218,253); alpha [1] */
+size_t ctn_prelu_workspace_bytes(const ctn_rows_desc* d);
+int ctn_prelu_forward(const ctn_rows_desc* d, const void* x, const float* alpha, void* y, void* stream);
+int ctn_prelu_backward(const ctn_rows_desc* d, const void* x, const float* alpha, const void* gy, void* gx,
+                       float* galpha, void* ws, size_t ws_bytes, void* stream);
+
+/* depthwise Conv1d(C, C, P, dilation, groups=C, bias=False) with the reference's
+ * padding (conv_tasnet.py:188,262-265) and, causal, its Chomp1d (:275-289);
+ * w [C,1,P]; non-causal needs (P-1)*dilation even (output length K) */
+size_t ctn_depthwise_workspace_bytes(const ctn_rows_desc* d, int P);
+int ctn_depthwise_forward(const ctn_rows_desc* d, int P, int dilation, int causal, const void* x, const float* w,
+                          void* y, void* stream);
+int ctn_depthwise_backward(const ctn_rows_desc* d, int P, int dilation, int causal, const void* x, const float* w,
+                           const void* gy, void* gx, float* gw, void* ws, size_t ws_bytes, void* stream);
+
+/* Conv1d(C, cout, 1, bias=False) (conv_tasnet.py:169,185,215,270); w [cout,C,1];
+ * C and cout multiples of 8 */
+size_t ctn_conv1x1_workspace_bytes(const ctn_rows_desc* d, int cout, int backward);
+int ctn_conv1x1_forward(const ctn_rows_desc* d, int cout, const void* x, const float* w, void* y, void* ws,
+                        size_t ws_bytes, void* stream);
+int ctn_conv1x1_backward(const ctn_rows_desc* d, int cout, const void* x, const float* w, const void* gy, void* gx,
+                         float* gw, void* ws, size_t ws_bytes, void* stream);
+
+/* mask nonlinearity (conv_tasnet.py:202-208) over nspk speakers of score rows
+ * [M*Kp][nspk*N] (d->C = nspk*N, channel s*N + n as score.view(M, C, N, K)) */
+int ctn_mask_forward(const ctn_rows_desc* d, int nspk, int mask_type, const void* score, void* mask, void* stream);
+int ctn_mask_backward(const ctn_rows_desc* d, int nspk, int mask_type, const void* score, const void* gmask,
+                      void* gscore, void* stream);
 
 /* -------------------------------------------------------------------------
  * Opt-in kernel timer (bench.py roofline): when enabled, every launch of the
