@@ -181,7 +181,12 @@ def main():
     model = ct.ConvTasNet(**cfg).to(dev)
     model.act_dtype = torch.float32 if args.fp32 else torch.bfloat16
     if use_ddp:
-        model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], bucket_cap_mb=25)
+        # gradients as views into the RCCL buckets (no per-step copy into the buckets),
+        # one fixed graph (the reducer skips its unused-parameter search each step)
+        model = torch.nn.parallel.DistributedDataParallel(
+            model, device_ids=[local], bucket_cap_mb=int(os.environ.get("CTN_DDP_BUCKET_MB", "25")),
+            gradient_as_bucket_view=os.environ.get("CTN_DDP_VIEW", "1") == "1",
+            static_graph=os.environ.get("CTN_DDP_STATIC", "1") == "1")
     # the solver's update (src/solver.py:184-186) on the HIP path: one launch for
     # the clip norm, one for the clip scale, one for Adam over all 294 tensors
     opt = ctn_optim.Adam(model.parameters(), lr=1e-3)

@@ -215,13 +215,14 @@ GemmRows tb_gemmB(const ctn_tblock_desc* d, bool fused) {
   return g;
 }
 // The norm-1/PReLU-1 backward runs inside the first 1x1's two gradient GEMMs (bf16,
-// gLN, weight-stationary data-gradient kernel, dual pair B off); else norm1_bwd_kernel.
+// gLN or cLN, weight-stationary data-gradient kernel, dual pair B off); else
+// norm1_bwd_kernel.
 // CTN_FUSE_N1=0 keeps the separate kernel (read on every query, so a process can
 // compare both paths: tests/test_gpu_tblock.py).
 bool tb_fused_n1(const ctn_tblock_desc* d) {
   const char* e = getenv("CTN_FUSE_N1");
   if (e && atoi(e) == 0) return false;
-  if (d->dtype != CTN_DTYPE_BF16 || d->norm_type != CTN_NORM_GLN) return false;
+  if (d->dtype != CTN_DTYPE_BF16 || (d->norm_type != CTN_NORM_GLN && d->norm_type != CTN_NORM_CLN)) return false;
   if (gemm_dual_eligible(BF16, tb_dualB(d))) return false;
   GemmRows g = tb_gemmB(d, true);
   static const float dummy[2] = {0.f, 0.f};   // eligibility only checks presence
@@ -597,6 +598,10 @@ extern "C" int ctn_tblock_forward(const ctn_tblock_desc* d, const ctn_tblock_par
   da.alpha1 = p->alpha1; da.gamma1 = p->gamma1; da.beta1 = p->beta1; da.alpha2 = p->alpha2;
   da.wd = p->wd; da.d_out = sv->d; da.slab2 = L.slab2;
   if (fold) da.f_st1 = gemm_rows_stat_fold(dt, g1, L.slab1, cnt, (float)kEps, 0, st1);
+  if (d->norm_type == CTN_NORM_CLN) {   // per-row statistics final in the depthwise kernel
+    da.st2_out = st2;
+    da.eps = (float)kEps;
+  }
   {
     TimedScope ts(2, s);
     CTN_HIP(launch_dw_fwd(dt, da, s));
@@ -611,7 +616,7 @@ extern "C" int ctn_tblock_forward(const ctn_tblock_desc* d, const ctn_tblock_par
   g2.epi = EPI_RESID; g2.R = x; g2.ldr = d->B;
   g2.C = y; g2.ldc = d->B;
   if (fold && gemm_ws_can_fold(dt, g2)) g2.aop.fold = StatFold{L.slab2, L.parts2, cnt, (float)kEps, 0, st2};
-  else CTN_HIP(launch_stats_finalize(L.slab2, G, L.parts2, cnt, 0, (float)kEps, st2, s));
+  else if (!da.st2_out) CTN_HIP(launch_stats_finalize(L.slab2, G, L.parts2, cnt, 0, (float)kEps, st2, s));
   CTN_HIP(launch_gemm_rows(dt, g2, s));
   return CTN_OK;
 }
@@ -693,8 +698,10 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
   if (fold)
     da.f_sm2 = dualA ? gemm_dual_stat_fold(duA, L.slabA, cnt, 0.f, 1, nullptr)
                      : gemm_rows_stat_fold(dt, ga, L.slabA, cnt, 0.f, 1, nullptr);
+  else
+    da.sm1_out = L.sums1;   // cLN: per-row norm-1 backward means final in the depthwise kernel
   CTN_HIP(launch_dw_bwd(dt, da, s));
-  const bool fused1 = fold && tb_fused_n1(d);
+  const bool fused1 = tb_fused_n1(d);
   int nalpha = ew_blocks(da);
   if (fused1) {
     // (d+e) gx = n1bwd(G2) . W1 + gy; the operand stage applies the norm-1/PReLU-1
@@ -705,7 +712,8 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
     gb.A = L.G2; gb.W = w1t; gb.R = gy; gb.C = gx;
     gb.aop.stats = st1; gb.aop.alpha = p->alpha1; gb.aop.aux = sv->h1; gb.aop.apart = L.alphaSlab;
     gb.aop.aout = L.G1;
-    gb.aop.fold = StatFold{L.slabD, L.partsD, cnt, 0.f, 1, nullptr};
+    if (fold) gb.aop.fold = StatFold{L.slabD, L.partsD, cnt, 0.f, 1, nullptr};
+    else gb.aop.sums = L.sums1;
     CTN_HIP(launch_gemm_rows(dt, gb, s));
     nalpha = gemm_ws_grid(gb);
     // (f) dW1 = gh1^T . x, gh1 = G1 as stored by the kernel above
@@ -716,7 +724,6 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
     c1.Cpart = L.cpart1; c1.nchunks = L.chunks1;
     CTN_HIP(launch_gemm_cols(dt, c1, s));
   } else {
-    if (!fold) CTN_HIP(launch_stats_finalize(L.slabD, G, L.partsD, cnt, 1, 0.f, L.sums1, s));
     // (d) norm1 backward finish + PReLU1 backward -> G1 = dL/dh1
     DwArgs de = da;
     de.ga2 = L.G2; de.sm1 = L.sums1; de.gh1_out = L.G1; de.alpha_slab = L.alphaSlab;

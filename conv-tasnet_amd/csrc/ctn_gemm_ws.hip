@@ -190,6 +190,7 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
   // the tile loop is unrolled by PF).
   v4u ra[PF][NA];
   float2 ast[PF][NA];
+  float2 asm1[PF][N1B && NK == NORM_CLN ? NA : 1];   // N1B, cLN: per-row norm-1 backward means
   auto load_a = [&](int t, auto slot) __attribute__((always_inline)) {
     constexpr int s = decltype(slot)::value;
 #pragma unroll
@@ -199,6 +200,7 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
       else ra[s][j] = ldg16(A + (size_t)r * p.lda + kc * 8);
       if constexpr (N1B) rh[s][j] = ldg16(H1 + (size_t)r * p.lda + kc * 8);
       if constexpr (OPK != OP_PLAIN && !FOLDS) ast[s][j] = p.aop.stats[stat_index<NK>(r, Kp)];
+      if constexpr (N1B && NK == NORM_CLN) asm1[s][j] = p.aop.sums[r];
     }
   };
   // ra -> LDS image of tile t (fragment (mb, kb) at (mb*KB + kb) KiB).  Rows of padded
@@ -217,8 +219,15 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
       const int r = rl0 + j * RSTEP;
       if constexpr (N1B) {
         // same arithmetic as norm1_bwd_kernel (ctn_tcn.hip), element by element
-        const int m = (t * TM) / Kp;
-        const float2 sm = sst[m], st = sst1[m];
+        float2 sm, st;
+        if constexpr (NK == NORM_GLN) {
+          const int m = (t * TM) / Kp;
+          sm = sst[m];
+          st = sst1[m];
+        } else {   // cLN: per-row statistics and means, loaded with the row
+          sm = asm1[s][j];
+          st = ast[s][j];
+        }
         float g[8], h[8];
         unpack_bf16x8(v, g);
         unpack_bf16x8(rh[s][j], h);
@@ -582,8 +591,9 @@ bool gemm_ws_eligible(DType dt, const GemmRows& p) {
   if (p.g.Kp % WS_TM || p.lda % 8 || p.ldw % 8 || p.ldc % 8) return false;
   if ((p.epi == EPI_RESID || p.epi == EPI_NORM_BWD) && p.ldr % 8) return false;
   if (p.aop.kind != OP_PLAIN && p.aop.norm == NORM_GLN && p.g.M > WS_FOLD_MAX) return false;
-  if (p.aop.kind == OP_NORM1_BWD && (p.aop.norm != NORM_GLN || !p.aop.aux || !p.aop.aout || !p.aop.apart ||
-                                     !p.aop.stats || (!p.aop.fold.slab && !p.aop.sums)))
+  if (p.aop.kind == OP_NORM1_BWD && (!p.aop.aux || !p.aop.aout || !p.aop.apart || !p.aop.stats ||
+                                     (!p.aop.fold.slab && !p.aop.sums) ||
+                                     (p.aop.norm == NORM_CLN && !p.aop.sums)))
     return false;
   return true;
 }
@@ -658,10 +668,7 @@ static hipError_t ws_launch_shape(const GemmRows& p, hipStream_t s) {
 template <int NK>
 static hipError_t ws_launch_nk(const GemmRows& p, hipStream_t s) {
   if (p.aop.kind == OP_PRELU_NORM) return ws_launch_shape<OP_PRELU_NORM, NK, EPI_RESID>(p, s);
-  if (p.aop.kind == OP_NORM1_BWD) {
-    if constexpr (NK == NORM_GLN) return ws_launch_shape<OP_NORM1_BWD, NK, EPI_RESID>(p, s);
-    return hipErrorInvalidValue;
-  }
+  if (p.aop.kind == OP_NORM1_BWD) return ws_launch_shape<OP_NORM1_BWD, NK, EPI_RESID>(p, s);
   if (p.aop.kind == OP_NORM) return ws_launch_shape<OP_NORM, NK, EPI_STORE>(p, s);
   switch (p.epi) {
     case EPI_PRELU_STATS: return ws_launch_shape<OP_PLAIN, NK, EPI_PRELU_STATS>(p, s);

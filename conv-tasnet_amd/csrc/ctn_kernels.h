@@ -174,6 +174,12 @@ struct DwArgs {
   float* alpha_slab;                     // (ew) [blocks] galpha1 partials
   // gLN folds (StatFold): dw_fwd finalizes st1, dw_bwd sm2, norm1_bwd sm1
   StatFold f_st1, f_sm2, f_sm1;
+  // cLN: a lane group holds all H channels of a row, so the per-row statistics are
+  // final in-kernel: dw_fwd writes norm-2 (mean, rstd) to st2_out, dw_bwd the norm-1
+  // backward means to sm1_out (instead of slab partials + a finalize launch)
+  float eps = 0.f;
+  float2* st2_out = nullptr;
+  float2* sm1_out = nullptr;
 };
 int dw_seg(const DwArgs& a, bool bwd);   // comb segment length sizing one resident round
 int dw_blocks(const DwArgs& a);        // depthwise (comb) kernels (a.seg set)

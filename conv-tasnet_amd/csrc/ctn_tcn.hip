@@ -212,7 +212,16 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
     } else {
       s = wave_sum_group(s, gm.cg);
       ss = wave_sum_group(ss, gm.cg);
-      if (c == 0 && k < Kp) a.slab2[it.base + k] = make_double2((double)s, (double)ss);
+      if (c == 0 && k < Kp) {
+        if (a.st2_out) {   // final (mean, rstd), the arithmetic of stats_finalize (mode 0)
+          const double mean = (double)s / H;
+          double var = (double)ss / H - mean * mean;
+          if (var < 0.0) var = 0.0;
+          a.st2_out[it.base + k] = make_float2((float)mean, (float)(1.0 / sqrt(var + (double)a.eps)));
+        } else {
+          a.slab2[it.base + k] = make_double2((double)s, (double)ss);
+        }
+      }
     }
 #pragma unroll
     for (int i = 0; i < P - 1; ++i)
@@ -379,7 +388,12 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
     } else {
       s = wave_sum_group(s, gm.cg);
       ss = wave_sum_group(ss, gm.cg);
-      if (c == 0 && k < Kp) a.slab1[it.base + k] = make_double2((double)s, (double)ss);
+      if (c == 0 && k < Kp) {
+        if (a.sm1_out)   // final means, the arithmetic of stats_finalize (mode 1)
+          a.sm1_out[it.base + k] = make_float2((float)((double)s / H), (float)((double)ss / H));
+        else
+          a.slab1[it.base + k] = make_double2((double)s, (double)ss);
+      }
     }
 #pragma unroll
     for (int i = 0; i < P - 1; ++i) {

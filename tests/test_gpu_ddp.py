@@ -57,7 +57,7 @@ def _step(model, mix, src, bf16):
     return float(loss), grads, [p.detach().cpu().clone() for p in model.parameters()]
 
 
-def _worker(rank, world, port, bf16, q):
+def _worker(rank, world, port, bf16, view, q):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -66,7 +66,9 @@ def _worker(rank, world, port, bf16, q):
         dev = torch.device("cuda", 0)
         torch.manual_seed(0)
         model = ct.ConvTasNet(**CFG).to(dev)
-        ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[0], bucket_cap_mb=0.1)
+        # view: the bench / train.py options (gradients as bucket views, static graph)
+        ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[0], bucket_cap_mb=0.1,
+                                                        gradient_as_bucket_view=view, static_graph=view)
         mix, src = _batch()
         shard = slice(rank * (M // world), (rank + 1) * (M // world))
         loss, grads, params = _step(ddp, mix[shard].to(dev), src[shard].to(dev), bf16)
@@ -77,13 +79,13 @@ def _worker(rank, world, port, bf16, q):
 
 
 @pytest.mark.timeout(400)
-@pytest.mark.parametrize("bf16", [False, True])
-def test_ddp_two_ranks_hip_model_matches_full_batch(bf16):
+@pytest.mark.parametrize("bf16,view", [(False, False), (True, False), (False, True)])
+def test_ddp_two_ranks_hip_model_matches_full_batch(bf16, view):
     import conv_tasnet as ct
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, bf16, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, bf16, view, q)) for r in range(2)]
     for p in procs:
         p.start()
     try:

@@ -165,15 +165,16 @@ def test_dual_gemm_matches_four_kernel_path(d, causal, norm, monkeypatch):
         assert e < 5e-3 or (a.numel() == 1 and abs(float(a - b)) < 1e-2 * (1 + abs(float(b)))), (n, errs)
 
 
-@pytest.mark.parametrize("d,causal", [(2, 0), (32, 1), (1, 0)])
-def test_fused_norm1_backward_matches_separate_kernel(d, causal, monkeypatch):
-    """bf16 gLN: the norm-1/PReLU-1 backward applied inside the gx and dW1 GEMMs'
-    operand stages (OP_NORM1_BWD, ctn_gemm_ws.hip / ctn_gemm.hip) gives the results of
-    the separate norm1_bwd kernel: the same per-element arithmetic on the same bf16
-    inputs, so gx and dW1 agree up to fp32 rounding, and the PReLU-1 alpha gradient
-    up to its summation order."""
+@pytest.mark.parametrize("d,causal,norm", [(2, 0, "gLN"), (32, 1, "gLN"), (1, 0, "gLN"), (4, 1, "cLN"),
+                                           (64, 1, "cLN"), (2, 0, "cLN")])
+def test_fused_norm1_backward_matches_separate_kernel(d, causal, norm, monkeypatch):
+    """bf16 gLN / cLN: the norm-1/PReLU-1 backward applied inside the gx GEMM's
+    operand stage (OP_NORM1_BWD, ctn_gemm_ws.hip; cLN with per-row statistics and
+    means) gives the results of the separate norm1_bwd kernel: the same per-element
+    arithmetic on the same bf16 inputs, so gx and dW1 agree up to fp32 rounding, and
+    the PReLU-1 alpha gradient up to its summation order."""
     torch.manual_seed(1)
-    params = _paper_block(5, causal=bool(causal), norm="gLN")
+    params = _paper_block(5, causal=bool(causal), norm=norm)
     M, B, K = 3, 256, 1000
     x = torch.randn(M, B, K)
     G = torch.randn(M, B, K)
@@ -181,10 +182,10 @@ def test_fused_norm1_backward_matches_separate_kernel(d, causal, monkeypatch):
     outs = []
     for flag in ("0", "1"):
         monkeypatch.setenv("CTN_FUSE_N1", flag)
-        outs.append(run_block(x, params, 3, d, causal, "gLN", G, torch.bfloat16)[:3])
+        outs.append(run_block(x, params, 3, d, causal, norm, G, torch.bfloat16)[:3])
     (y0, gx0, gp0), (y1, gx1, gp1) = outs
     errs = {n: rel(a, b) for n, a, b in zip(_names(causal), gp1, gp0)}
-    print(causal, d, "gx", rel(gx1, gx0), errs)
+    print(norm, causal, d, "gx", rel(gx1, gx0), errs)
     assert torch.equal(y0, y1)
     assert rel(gx1, gx0) < 2e-3
     for (n, e), a, b in zip(errs.items(), gp1, gp0):
