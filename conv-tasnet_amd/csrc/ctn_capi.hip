@@ -583,13 +583,20 @@ extern "C" int ctn_tblock_forward(const ctn_tblock_desc* d, const ctn_tblock_par
   g1.alpha = p->alpha1;
   g1.C = sv->h1;
   g1.grp_slab = L.slab1;
+  // cLN on the WS kernel: the workgroup holds all H channels of its rows and writes
+  // the final per-row statistics itself
+  const bool fin1 = d->norm_type == CTN_NORM_CLN && gemm_ws_final_cln(dt, g1);
+  if (fin1) {
+    g1.stats_out = st1;
+    g1.eps = (float)kEps;
+  }
   {
     TimedScope ts(1, s);
     CTN_HIP(launch_gemm_rows(dt, g1, s));
   }
   // gLN: the consumers finalize the statistics from the slab partials (StatFold)
   const bool fold = d->norm_type == CTN_NORM_GLN;
-  if (!fold) CTN_HIP(launch_stats_finalize(L.slab1, G, L.parts1, cnt, 0, (float)kEps, st1, s));
+  if (!fold && !fin1) CTN_HIP(launch_stats_finalize(L.slab1, G, L.parts1, cnt, 0, (float)kEps, st1, s));
   // norm1 apply + depthwise dilated conv, PReLU statistics for norm2
   DwArgs da{};
   da.g = rg; da.H = d->H; da.P = d->P; da.dil = d->dilation; da.pad = tb_pad(d); da.norm = d->norm_type;

@@ -64,7 +64,7 @@ constexpr int WS_FOLD_MAX = 512;   // utterances whose gLN operand stats a workg
 #endif
 // LDS fragment look-ahead of the MFMA loop, in k-steps
 #ifndef CTN_WS_LA16
-#define CTN_WS_LA16 1
+#define CTN_WS_LA16 0
 #endif
 #ifndef CTN_WS_LA8
 #define CTN_WS_LA8 3
@@ -104,6 +104,10 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
   constexpr bool N1B = OPK == OP_NORM1_BWD;    // norm-1/PReLU-1 backward on the operand
   constexpr bool SWP = OPK == OP_PLAIN && WV == 8;
   constexpr int PF = SWP ? 1 : (WV == 16 ? CTN_WS_PF16 : CTN_WS_PF8);
+  // cLN PReLU statistics finalized in the kernel: per-row partials of the WV waves of
+  // one tile meet in LDS and are summed after the next barrier (tile parity buffers)
+  constexpr bool CLN_FIN = EPI == EPI_PRELU_STATS && NK == NORM_CLN && !SWP && S == 1;
+  __shared__ double2 scln[CLN_FIN ? 2 * TM * WV : 1];
   __shared__ __attribute__((aligned(16))) char sA[2][TM * KR * 2];
   __shared__ float sgam[EPI == EPI_NORM_BWD ? NB * 16 * WV : 1];
   // gLN operand statistics, one pair per utterance, finalized here (StatFold)
@@ -431,7 +435,11 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
           float s = s2[0] + s2[1], ss = q2[0] + q2[1];
           s += __shfl_xor(s, 16, 64); ss += __shfl_xor(ss, 16, 64);
           s += __shfl_xor(s, 32, 64); ss += __shfl_xor(ss, 32, 64);
-          p.grp_slab[(size_t)r * (S * WV) + wslot] = make_double2((double)s, (double)ss);
+          if (CLN_FIN && p.stats_out) {
+            if (lg == 0) scln[((t & 1) * TM + mb * 16 + lr) * WV + wid] = make_double2((double)s, (double)ss);
+          } else {
+            p.grp_slab[(size_t)r * (S * WV) + wslot] = make_double2((double)s, (double)ss);
+          }
         }
       }
     }
@@ -450,6 +458,25 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
   auto epilogue = [&](auto le1, int t, const f32x4_t (&acc)[MB][NB]) __attribute__((always_inline)) {
     epilogue_math(le1, t, acc);
     store_out(t);
+  };
+  // cLN: final (mean, rstd) of tile t's rows from the WV wave partials, summed in wave
+  // order in fp64 (the arithmetic of stats_finalize over this layout's parts)
+  auto cln_final = [&](int t) __attribute__((always_inline)) {
+    if constexpr (CLN_FIN) {
+      if (p.stats_out && tid < TM) {
+        double sm = 0.0, sq = 0.0;
+#pragma unroll 1
+        for (int w = 0; w < WV; ++w) {
+          const double2 v = scln[((t & 1) * TM + tid) * WV + w];
+          sm += v.x;
+          sq += v.y;
+        }
+        const double mean = sm / p.Nout;
+        double var = sq / p.Nout - mean * mean;
+        if (var < 0.0) var = 0.0;
+        p.stats_out[(size_t)t * TM + tid] = make_float2((float)mean, (float)(1.0 / sqrt(var + (double)p.eps)));
+      }
+    }
   };
 
 #pragma unroll
@@ -487,6 +514,7 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
           const int t = tb + decltype(u)::value;
           if (PF == 1 || t < t1) {
             lds_barrier();
+            if (t > t0) cln_final(t - 1);
             mfma_tile(sA[t & 1], acc);
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (CTN_WS_ORDER == 1) {
@@ -547,6 +575,10 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
     run(std::true_type{});
   }
   if constexpr (HAS_STATS && NK == NORM_GLN) flush_run();
+  if constexpr (CLN_FIN) {
+    lds_barrier();
+    cln_final(t1 - 1);
+  }
   if constexpr (N1B) {   // fixed-order workgroup sum of the alpha-gradient partials
     const float w = wave_sum_dpp(calpha);
     if (lane == 0) salpha[wid] = w;
@@ -596,6 +628,15 @@ bool gemm_ws_eligible(DType dt, const GemmRows& p) {
                                      (p.aop.norm == NORM_CLN && !p.aop.sums)))
     return false;
   return true;
+}
+
+static int ws_slices(const GemmRows& p);
+static int ws_waves(const GemmRows& p);
+bool gemm_ws_final_cln(DType dt, const GemmRows& p) {
+  // the 16-wave (non-interleaved, one slice) configuration of Nout = 512 or the 8-wave
+  // Nout = 512 norm-backward one: every wave's partial meets in one workgroup
+  return gemm_ws_eligible(dt, p) && p.epi == EPI_PRELU_STATS && p.norm == NORM_CLN && p.aop.kind == OP_PLAIN &&
+         p.Nout == 512 && p.Kred == 256 && ws_slices(p) == 1;
 }
 
 bool gemm_ws_can_fold(DType dt, const GemmRows& p) {

@@ -58,6 +58,10 @@ struct GemmRows {
   const float* gamma = nullptr;           // EPI_NORM_BWD gamma
   int norm = 0;                           // NormKind for the epilogue statistics
   double2* grp_slab = nullptr;            // group partials
+  // EPI_PRELU_STATS, cLN, WS kernel (gemm_ws_final_cln): per-row (mean, rstd) of the
+  // output written here directly (the workgroup holds every channel of its rows)
+  float2* stats_out = nullptr;
+  float eps = 0.f;
 };
 // Slab sizing must be queried with the same GemmRows (shape, operand op, epilogue,
 // strides) that is later launched: the kernel choice decides the part counts.
@@ -72,6 +76,7 @@ WsRuns gemm_ws_runs(const GemmRows& p);
 StatFold gemm_rows_stat_fold(DType dt, const GemmRows& p, const double2* slab, double cnt, float eps, int mode,
                              float2* out);
 bool gemm_ws_can_fold(DType dt, const GemmRows& p);   // WS kernel and its operand stats fit the fold
+bool gemm_ws_final_cln(DType dt, const GemmRows& p);  // WS kernel writes final cLN stats (stats_out)
 hipError_t launch_gemm_ws(const GemmRows& p, hipStream_t s);
 
 // ---- column GEMM (weight gradient): Cpart[chunk][p][q] = sum_r opA(A[r][p]) * opB(B[r][q])
