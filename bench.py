@@ -235,11 +235,15 @@ def main():
         kb = kernel_bytes(args.timer_kind, M, K, cfg, s)
         mean_ms = tot.value / max(nl.value, 1)
         achieved = kb / (mean_ms * 1e-3) / 1e9
-        traffic = None
+        traffic = mfma = None
         pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc):
             with open(pmc) as f:
                 traffic = json.load(f).get(str(args.timer_kind))
+        pmc = os.path.join(ROOT, "profiles", "pmc_mfma.json")   # tools/gpu_round2.sh MFMA pass
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                mfma = json.load(f).get(str(args.timer_kind))
         out = {
             "metric": "utterances/sec (4s, 8kHz, 2-spk) fwd+bwd",
             "value": round(utt_s, 2),
@@ -269,7 +273,12 @@ def main():
                                     3: ("gemm_dual bwd g_n2 = gy.W2 (norm-backward epilogue) + dW2 = gy^T.n2"
                                         if dual_pair_a() else
                                         "gemm_rows bwd g_n2 = gy.W2 (norm-backward epilogue)")}[args.timer_kind],
-                         "launches": nl.value, "mean_ms": round(mean_ms, 4), "bytes_per_launch": kb},
+                         "launches": nl.value, "mean_ms": round(mean_ms, 4), "bytes_per_launch": kb,
+                         # rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * 1024 SIMDs) of
+                         # this kernel, from the committed PMC pass (profiles/pmc_mfma.json)
+                         "mfma_util": mfma.get("mfma_util") if mfma else None,
+                         # the whole step against the same peak: SURVEY §8d compulsory bytes
+                         "step_frac": round(step_alg_bytes(M, K, T, cfg, s) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
             "step_model": {"alg_bytes_GB": round(step_alg_bytes(M, K, T, cfg, s) / 1e9, 3),
                            "alg_GBps": round(step_alg_bytes(M, K, T, cfg, s) / (ms * 1e-3) / 1e9, 1),
                            "tflops": round(step_flops(M, K, cfg) / (ms * 1e-3) / 1e12, 1)},

@@ -8,6 +8,12 @@ WAIT_INST_ANY (issue stall), ACTIVE_INST_ANY (issuing)."""
 import csv, glob, os, sys
 from collections import defaultdict
 root = sys.argv[1]
+json_out = sys.argv[2] if len(sys.argv) > 2 else None
+KINDS = {   # bench.py timer kinds -> kernel name (bf16 throughput mode)
+    "1": "gemm_ws_kernel<0, 0, 1, 2, 8, 16, 2, 1>",
+    "2": "dw_fwd_kernel<unsigned short, 0, 3, false>",
+    "3": "gemm_dual_kernel<8, 8, 2, 3, 2, 0, 4>",
+}
 vals = defaultdict(lambda: defaultdict(list))
 for f in sorted(glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)):
     for r in csv.DictReader(open(f)):
@@ -33,3 +39,15 @@ for k, d in vals.items():
         m(d, "SQ_INSTS_LDS") / mf if mf else float("nan"))))
 for _, r in sorted(rows, reverse=True):
     print(r)
+if json_out:
+    import json
+    out = {}
+    for kind, pat in KINDS.items():
+        for k, d in vals.items():
+            if k.startswith(pat) or k == pat:
+                cyc = m(d, "GRBM_GUI_ACTIVE") / 8.0
+                busy = m(d, "SQ_VALU_MFMA_BUSY_CYCLES")
+                out[kind] = {"kernel": k, "mfma_util": round(busy / (cyc * 1024), 4), "mfma_per_launch": m(d, "SQ_INSTS_MFMA"),
+                             "mfma_busy_cycles": busy, "gui_active_per_xcd": cyc,
+                             "note": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 XCDs * 1024 SIMDs), per launch"}
+    json.dump(out, open(json_out, "w"), indent=1)
