@@ -200,9 +200,44 @@ CTN_DEV float wave_sum_dpp(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
 }
 
+// fp64 wave64 sum with the same DPP row operations on both halves (no ds_bpermute:
+// kernels with LDS-DMA in flight reduce this way; total read from lane 63)
+template <int CTRL, int ROW_MASK> CTN_DEV double dpp_d(double x) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, x);
+  const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)b, CTRL, ROW_MASK, 0xF, false);
+  const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), CTRL, ROW_MASK, 0xF, false);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+CTN_DEV double wave_sum_dpp_d(double v) {
+  v += dpp_d<0xB1, 0xF>(v);
+  v += dpp_d<0x4E, 0xF>(v);
+  v += dpp_d<0x141, 0xF>(v);
+  v += dpp_d<0x140, 0xF>(v);
+  v += dpp_d<0x142, 0xA>(v);
+  v += dpp_d<0x143, 0xC>(v);
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, 63);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), 63);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
 // float2 (packed fp32: v_pk_add/mul/fma_f32 on gfx950) helpers
+// IEEE maximum/minimum (NaN-propagating): one v_maximum3/v_minimum3_f32 per element on
+// gfx950, where maxnum/minnum in IEEE mode also quiet each non-arithmetic input first
+// (two more v_max_f32 per element)
+// 0 (default): maxnum/minnum as before.  1 measured neutral (fwd1 51.5 -> 51.2 us) and,
+// in the dual GEMM, moved code placement into the latent statistics race noted in
+// DESIGN.md §10
+#ifndef CTN_IEEE_MAX
+#define CTN_IEEE_MAX 0
+#endif
+#if CTN_IEEE_MAX
+CTN_DEV f32x2_t pmax(f32x2_t a, f32x2_t b) { return __builtin_elementwise_maximum(a, b); }
+CTN_DEV f32x2_t pmin(f32x2_t a, f32x2_t b) { return __builtin_elementwise_minimum(a, b); }
+#else
 CTN_DEV f32x2_t pmax(f32x2_t a, f32x2_t b) { return __builtin_elementwise_max(a, b); }
 CTN_DEV f32x2_t pmin(f32x2_t a, f32x2_t b) { return __builtin_elementwise_min(a, b); }
+#endif
 CTN_DEV f32x2_t pfma(f32x2_t a, f32x2_t b, f32x2_t c) { return __builtin_elementwise_fma(a, b, c); }
 // PReLU of a pair with one shared alpha: max(x, a*x) when a <= 1, min(x, a*x) when a > 1
 // (both exact: the branch is chosen once per kernel, LE1 = (alpha <= 1))

@@ -85,6 +85,16 @@ template <int NK> CTN_DEV float2 ld_stat(const float2* s, int m, int row) {
   return NK == NORM_GLN ? s[m] : s[row];
 }
 
+// cLN per-row sums of a comb walk.  With H = 512 one wave owns one comb item (its 64
+// lanes hold all channels of each row), so a row's sums are reduced with DPP (no LDS
+// round trips), parked one row per lane, and every 64 rows each lane finishes the row
+// it holds: the fp64 finishing arithmetic runs once per 64 rows, not once per row.
+// Narrower H (several items per wave) reduces per row over the lane group as before.
+struct RowPark {
+  float s = 0.f, ss = 0.f;
+  int j0;   // comb step held by lane 0
+};
+
 // column-partial reduction: sum val[8] over the lanes that own channel group c, write H floats
 CTN_DEV void col_reduce8(float* buf, const float v[8], int rl, int c, int nrl, int cg, bool act, float* dst) {
   const int H = cg * 8;
@@ -184,6 +194,24 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
 #pragma unroll
   for (int q = 0; q < D; ++q) fetch(it.j0 + q + P - 1 - POWN, pre[q], pok[q], prow[q], pst[q]);
   float ts = 0.f, tss = 0.f;
+  const bool wave_item = gm.cg == 64;   // one comb item per wave (see RowPark)
+  const int lane = threadIdx.x & 63;
+  RowPark pk;
+  pk.j0 = it.j0;
+  // final (mean, rstd) or the (sum, sum sq) slab entry of the rows parked in lanes < n
+  auto park_flush = [&](int n) {
+    const int k = row_of(pk.j0 + lane);
+    if (lane < n && k < Kp) {
+      if (a.st2_out) {   // the arithmetic of stats_finalize (mode 0)
+        const double mean = (double)pk.s / H;
+        double var = (double)pk.ss / H - mean * mean;
+        if (var < 0.0) var = 0.0;
+        a.st2_out[it.base + k] = make_float2((float)mean, (float)(1.0 / sqrt(var + (double)a.eps)));
+      } else {
+        a.slab2[it.base + k] = make_double2((double)pk.s, (double)pk.ss);
+      }
+    }
+  };
   for (int jb = it.j0; jb < it.j1; jb += D)
 #pragma unroll
   for (int q = 0; q < D; ++q) {
@@ -211,6 +239,16 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
     if constexpr (NK == NORM_GLN) {
       ts += s;
       tss += ss;
+    } else if (wave_item) {
+      s = wave_sum_dpp(s);
+      ss = wave_sum_dpp(ss);
+      const int pq = j - pk.j0;
+      pk.s = lane == pq ? s : pk.s;
+      pk.ss = lane == pq ? ss : pk.ss;
+      if (pq == 63) {
+        park_flush(64);
+        pk.j0 = j + 1;
+      }
     } else {
       s = wave_sum_group(s, gm.cg);
       ss = wave_sum_group(ss, gm.cg);
@@ -230,6 +268,8 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) win[i][e] = win[i + 1][e];
   }
+  if constexpr (NK != NORM_GLN)
+    if (wave_item && it.j1 > pk.j0) park_flush(it.j1 - pk.j0);
   if constexpr (NK == NORM_GLN) {
     double v2[2] = {(double)ts, (double)tss};
     block_sum_d<2>(v2, red);
@@ -340,6 +380,20 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
     ahok[i] = okh;
   }
   constexpr int D = dw_pf<T>();   // rows in flight per lane, slots as in dw_fwd
+  const bool wave_item = gm.cg == 64;   // one comb item per wave (see RowPark)
+  const int lane = threadIdx.x & 63;
+  RowPark pk;
+  pk.j0 = it.j0;
+  // final norm-1 backward means or the slab entry of the rows parked in lanes < n
+  auto park_flush = [&](int n) {
+    const int k = row_of(pk.j0 + lane);
+    if (lane < n && k < Kp) {
+      if (a.sm1_out)   // the arithmetic of stats_finalize (mode 1)
+        a.sm1_out[it.base + k] = make_float2((float)((double)pk.s / H), (float)((double)pk.ss / H));
+      else
+        a.slab1[it.base + k] = make_double2((double)pk.s, (double)pk.ss);
+    }
+  };
   Raw8<T> pd[D], pg[D], ph[D]; bool pok[D], pokh[D]; int prow[D], prowh[D];
 #pragma unroll
   for (int q = 0; q < D; ++q) {
@@ -389,6 +443,16 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
     if constexpr (NK == NORM_GLN) {
       ts += s;
       tss += ss;
+    } else if (wave_item) {
+      s = wave_sum_dpp(s);
+      ss = wave_sum_dpp(ss);
+      const int pq = j - pk.j0;
+      pk.s = lane == pq ? s : pk.s;
+      pk.ss = lane == pq ? ss : pk.ss;
+      if (pq == 63) {
+        park_flush(64);
+        pk.j0 = j + 1;
+      }
     } else {
       s = wave_sum_group(s, gm.cg);
       ss = wave_sum_group(ss, gm.cg);
@@ -409,6 +473,8 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
       }
     }
   }
+  if constexpr (NK != NORM_GLN)
+    if (wave_item && it.j1 > pk.j0) park_flush(it.j1 - pk.j0);
   // ---- workgroup reductions: column partials, alpha2, norm1 sums
   const int cgn = gm.cg, nrl = 256 / cgn, rl = threadIdx.x / cgn;
   float* cs = a.col_slab + (size_t)blockIdx.x * dw_col_stride(a);

@@ -75,6 +75,20 @@ int main() {
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
     const double us = ms * 1e3 / NIT;
     printf("EXP %3d  %-30s %8.1f us  %7.0f GB/s\n", CTN_DU_EXP, c.name, us, c.bytes / us * 1e-3);
+#if CTN_DU_STAMP
+    {   // per-phase shares of the loop (diagnostic build: read shares, not lengths)
+      std::vector<unsigned long long> h(DU_GRID * DU_WV * 8);
+      CK(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(du_stamps), h.size() * 8));
+      const char* nm[8] = {"vmwait", "barrier", "store_c", "dma", "transform", "compute", "epilogue", "prologue"};
+      double sum[8] = {0}, tot = 0;
+      for (size_t w = 0; w < h.size() / 8; ++w)
+        for (int i = 0; i < 8; ++i) sum[i] += (double)h[w * 8 + i];
+      for (int i = 0; i < 7; ++i) tot += sum[i];
+      const int tiles = (int)(rows / DU_TM) / (DU_GRID / (c.g.Nout / (c.g.Kred == 256 ? 128 : 64)));
+      for (int i = 0; i < 8; ++i)
+        printf("   %-10s %5.1f %%  %8.0f cyc/tile/wave\n", nm[i], 100.0 * sum[i] / tot, sum[i] / (h.size() / 8) / tiles);
+    }
+#endif
   }
   if (CTN_DU_EXP == 0) {   // streaming calibration: copy d -> out (both rows x H bf16)
     const long n = rows * H * 2 / 16;
