@@ -8,10 +8,15 @@
 // dec_fwd     : frames[m][c][k][l] = sum_n (w[r][n] * act(score)[r][c][n]) V[l][n]   :128-140
 // ola_fwd     : est[m][c][t] = sum_{k: kS<=t<kS+L} frames[m][c][k][t-kS], zero to T  utils.py:9-46, :56-59
 // dec_bwd     : dL/dscore and dL/dw from dL/dest (frames gradient gathered from est)
+#include <stdlib.h>
+
 #include "ctn_common.h"
 #include "ctn_codec.h"
 
 namespace ctn {
+
+typedef short bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 constexpr int EN_RPB = 128;   // frame rows per workgroup (matches the row padding)
 
@@ -421,6 +426,225 @@ __global__ __launch_bounds__(256) void dec_bwd_kernel(CodecArgs a, int rpb) {
 }
 
 // ===========================================================================
+// bf16 decoder on the matrix cores (N = 32*KBN, L <= 32, C <= 4)
+//
+// Both directions are GEMMs with a short side (L, the basis length): the forward
+// frames[r,c,:] = src_c[r,:] . V^T with src_c = w * act(score_c), the backward
+// gsrc_c[r,:] = gframes_c[r,:] . V with gframes gathered from dL/dest.  The VALU
+// kernels above re-read V from LDS per output (LDS-bound, about 0.6 TB/s of the rows
+// they stream); here each workgroup converts the basis once into bf16 MFMA fragments
+// in LDS (lane-linear, one 16-byte read per fragment) and its waves stream 16-row
+// blocks of w and score straight from HBM into v_mfma_f32_16x16x32_bf16 operands
+// (the element-wise mask nonlinearity and product formed in fp32 on the way).  Waves are persistent and
+// walk blocks blk, blk + (all waves), ...; blocks never straddle utterances (Kp is a
+// multiple of 128).  Padded frames hold zero rows, so their outputs are zero and are
+// not stored (forward) or stored as the zeros they compute (backward).
+// ===========================================================================
+constexpr int DM_WAVES = 4;   // waves per workgroup
+
+// mask nonlinearity of C scores of one (row, channel), in place: relu / softmax / identity
+template <int CM> CTN_DEV void dm_act(int mask_type, int C, float (&x)[CM]) {
+  if (mask_type == 1) {
+    float mx = -3.4e38f, den = 0.f;
+#pragma unroll
+    for (int c = 0; c < CM; ++c)
+      if (c < C) mx = fmaxf(mx, x[c]);
+#pragma unroll
+    for (int c = 0; c < CM; ++c)
+      if (c < C) {
+        x[c] = __expf(x[c] - mx);
+        den += x[c];
+      }
+#pragma unroll
+    for (int c = 0; c < CM; ++c)
+      if (c < C) x[c] /= den;
+  } else if (mask_type == 0) {
+#pragma unroll
+    for (int c = 0; c < CM; ++c) x[c] = x[c] > 0.f ? x[c] : 0.f;
+  }
+}
+
+template <int KBN>
+__global__ __launch_bounds__(256) void dec_fwd_mfma_kernel(CodecArgs a) {
+  constexpr int N = KBN * 32, CM = 4;
+  __shared__ v4u bfrag[2 * KBN * 64];
+  const int lane = threadIdx.x & 63, lg = lane >> 4, wv = threadIdx.x >> 6;
+  const int L = a.L, C = a.C, K = a.K, Kp = a.Kp;
+  // basis fragments (B operand) [nb][kb][lane]: column l = nb*16 + (lane & 15),
+  // channels kb*32 + 8*(lane >> 4) .. +8
+  for (int i = threadIdx.x; i < 2 * KBN * 64; i += 256) {
+    const int ln = i & 63, kb = (i >> 6) % KBN, nb = i / (64 * KBN), l = nb * 16 + (ln & 15);
+    float f[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (l < L) Vec8<float>::load(a.V + (size_t)l * N + kb * 32 + 8 * (ln >> 4), f);
+    bfrag[i] = pack_bf16x8v(f);
+  }
+  __syncthreads();
+  const int lr = lane & 15;
+  const bf16raw* w = reinterpret_cast<const bf16raw*>(a.w_rows);
+  const bf16raw* sc = reinterpret_cast<const bf16raw*>(a.score);
+  const long nblk = (long)a.M * Kp / 16;
+  for (long blk = (long)blockIdx.x * DM_WAVES + wv; blk < nblk; blk += (long)gridDim.x * DM_WAVES) {
+    const long r0 = blk * 16;
+    const int m = (int)(r0 / Kp), k0 = (int)(r0 - (long)m * Kp);
+    if (k0 >= K) continue;   // a block of padded frames (wave-uniform)
+    const long r = r0 + lr;
+    f32x4_t acc[CM][2];
+#pragma unroll
+    for (int c = 0; c < CM; ++c) acc[c][0] = acc[c][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < KBN; ++kb) {
+      const int ch = kb * 32 + 8 * lg;
+      float wf[8], sf[CM][8];
+      unpack_bf16x8(ldg16(w + r * N + ch), wf);
+#pragma unroll
+      for (int c = 0; c < CM; ++c)
+        if (c < C) unpack_bf16x8(ldg16(sc + r * (long)(C * N) + (long)c * N + ch), sf[c]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float x[CM];
+#pragma unroll
+        for (int c = 0; c < CM; ++c) x[c] = c < C ? sf[c][e] : 0.f;
+        dm_act<CM>(a.mask_type, C, x);
+#pragma unroll
+        for (int c = 0; c < CM; ++c) sf[c][e] = wf[e] * x[c];
+      }
+#pragma unroll
+      for (int c = 0; c < CM; ++c)
+        if (c < C) {
+          const bf16x8_t af = __builtin_bit_cast(bf16x8_t, pack_bf16x8v(sf[c]));
+          const v4u b0 = bfrag[kb * 64 + lane], b1 = bfrag[(KBN + kb) * 64 + lane];
+          acc[c][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, __builtin_bit_cast(bf16x8_t, b0), acc[c][0], 0, 0, 0);
+          acc[c][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, __builtin_bit_cast(bf16x8_t, b1), acc[c][1], 0, 0, 0);
+        }
+    }
+    // lane holds frames (row 4lg + i, l = nb*16 + lr)
+#pragma unroll
+    for (int c = 0; c < CM; ++c)
+      if (c < C)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+          const int l = nb * 16 + lr;
+          if (l >= L) continue;
+          float* f = a.frames + (((size_t)m * C + c) * Kp + k0) * L + l;
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (k0 + 4 * lg + i < K) f[(size_t)(4 * lg + i) * L] = acc[c][nb][i];
+        }
+  }
+}
+
+template <int NBN>   // N / 16
+__global__ __launch_bounds__(256) void dec_bwd_mfma_kernel(CodecArgs a) {
+  constexpr int N = NBN * 16, CM = 4;
+  __shared__ v4u afrag[NBN * 64];
+  const int lane = threadIdx.x & 63, lr = lane & 15, lg = lane >> 4, wv = threadIdx.x >> 6;
+  const int L = a.L, C = a.C, S = a.S, K = a.K, Kp = a.Kp;
+  // basis fragments (A operand) [nb][lane]: row n = nb*16 + (lane & 15), k = l =
+  // 8*(lane >> 4) .. +8 (zero past L)
+  for (int i = threadIdx.x; i < NBN * 64; i += 256) {
+    const int ln = i & 63, nb = i >> 6;
+    float f[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int l = 8 * (ln >> 4) + j;
+      f[j] = l < L ? a.V[(size_t)l * N + nb * 16 + (ln & 15)] : 0.f;
+    }
+    afrag[i] = pack_bf16x8v(f);
+  }
+  __syncthreads();
+  const bf16raw* w = reinterpret_cast<const bf16raw*>(a.w_rows);
+  const bf16raw* sc = reinterpret_cast<const bf16raw*>(a.score);
+  bf16raw* gsc = reinterpret_cast<bf16raw*>(a.gscore);
+  bf16raw* gw = reinterpret_cast<bf16raw*>(a.gwdec_out);
+  const long nblk = (long)a.M * Kp / 16;
+  typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+  for (long blk = (long)blockIdx.x * DM_WAVES + wv; blk < nblk; blk += (long)gridDim.x * DM_WAVES) {
+    const long r0 = blk * 16;
+    const int m = (int)(r0 / Kp), k0 = (int)(r0 - (long)m * Kp);
+    // frames gradient (B operand): row r = lr (column of the product), l = 8lg .. +8
+    v4u gb[CM];
+    {
+      const int k = k0 + lr;
+#pragma unroll
+      for (int c = 0; c < CM; ++c) {
+        float f[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (c < C && k < K) {
+          const float* g = a.gest + ((size_t)m * C + c) * a.T + (long)k * S;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int l = 8 * lg + j;
+            if (l < L && (long)k * S + l < a.T) f[j] = g[l];
+          }
+        }
+        gb[c] = pack_bf16x8v(f);
+      }
+    }
+#pragma unroll 2
+    for (int nb = 0; nb < NBN; ++nb) {
+      // gsrc_c[row r0 + lr][n = nb*16 + 4lg + i]
+      f32x4_t gs[CM];
+#pragma unroll
+      for (int c = 0; c < CM; ++c)
+        if (c < C)
+          gs[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, afrag[nb * 64 + lane]),
+                                                        __builtin_bit_cast(bf16x8_t, gb[c]),
+                                                        f32x4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      const long r = r0 + lr;
+      const int n0 = nb * 16 + 4 * lg;
+      const v2u wr = *reinterpret_cast<const v2u*>(w + r * N + n0);
+      v2u sr[CM];
+#pragma unroll
+      for (int c = 0; c < CM; ++c)
+        if (c < C) sr[c] = *reinterpret_cast<const v2u*>(sc + r * (long)(C * N) + (long)c * N + n0);
+      float wf[4], gwv[4], go[CM][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t wd = wr[i >> 1];
+        wf[i] = __uint_as_float((i & 1) ? (wd & 0xffff0000u) : (wd << 16));
+        float s[CM], act[CM];
+#pragma unroll
+        for (int c = 0; c < CM; ++c) {
+          const uint32_t sd = c < C ? sr[c][i >> 1] : 0u;
+          s[c] = __uint_as_float((i & 1) ? (sd & 0xffff0000u) : (sd << 16));
+          act[c] = s[c];
+        }
+        dm_act<CM>(a.mask_type, C, act);
+        float gwe = 0.f, dot = 0.f, ga[CM];
+#pragma unroll
+        for (int c = 0; c < CM; ++c)
+          if (c < C) {
+            gwe += gs[c][i] * act[c];
+            ga[c] = gs[c][i] * wf[i];   // dL/d act_c
+            dot += ga[c] * act[c];
+          }
+        gwv[i] = gwe;
+#pragma unroll
+        for (int c = 0; c < CM; ++c)
+          if (c < C) go[c][i] = a.mask_type == 1 ? act[c] * (ga[c] - dot) : a.mask_type == 0 ? (s[c] > 0.f ? ga[c] : 0.f) : ga[c];
+      }
+#pragma unroll
+      for (int c = 0; c < CM; ++c)
+        if (c < C)
+          *reinterpret_cast<v2u*>(gsc + r * (long)(C * N) + (long)c * N + n0) =
+              v2u{pk_bf16(go[c][0], go[c][1]), pk_bf16(go[c][2], go[c][3])};
+      *reinterpret_cast<v2u*>(gw + r * N + n0) = v2u{pk_bf16(gwv[0], gwv[1]), pk_bf16(gwv[2], gwv[3])};
+    }
+  }
+}
+
+// CTN_DEC_MFMA=0 keeps the VALU decoder kernels for bf16 too (read per launch: A/B)
+static bool dec_mfma(DType dt, const CodecArgs& a) {
+  const char* e = getenv("CTN_DEC_MFMA");
+  if (e && atoi(e) == 0) return false;
+  return dt == BF16 && (a.N == 256 || a.N == 512) && a.L <= 32 && a.C <= 4;
+}
+static unsigned dm_grid(const CodecArgs& a) {
+  const long waves = (long)a.M * a.Kp / 16;
+  long wgs = (waves + DM_WAVES - 1) / DM_WAVES;
+  return (unsigned)(wgs < 1024 ? wgs : 1024);
+}
+
+// ===========================================================================
 // launchers
 // ===========================================================================
 static bool codec_ok(const CodecArgs& a) {
@@ -481,7 +705,10 @@ hipError_t launch_dec_fwd(DType dt, const CodecArgs& a, hipStream_t s) {
   const int rpb = dec_rpb(a);
   const size_t lds = (((size_t)a.N * a.L + 3) & ~(size_t)3) * 4 + (size_t)rpb * a.C * a.N * 4;
   const dim3 g((unsigned)((long)a.M * a.Kp / rpb)), b(256);
-  if (dt == BF16) hipLaunchKernelGGL(dec_fwd_kernel<bf16raw>, g, b, lds, s, a, rpb);
+  if (dec_mfma(dt, a)) {
+    if (a.N == 256) hipLaunchKernelGGL(dec_fwd_mfma_kernel<8>, dim3(dm_grid(a)), b, 0, s, a);
+    else hipLaunchKernelGGL(dec_fwd_mfma_kernel<16>, dim3(dm_grid(a)), b, 0, s, a);
+  } else if (dt == BF16) hipLaunchKernelGGL(dec_fwd_kernel<bf16raw>, g, b, lds, s, a, rpb);
   else hipLaunchKernelGGL(dec_fwd_kernel<float>, g, b, lds, s, a, rpb);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -497,7 +724,10 @@ hipError_t launch_dec_bwd(DType dt, const CodecArgs& a, hipStream_t s) {
   const int rpb = 32;
   const size_t lds = (((size_t)a.N * a.L + 3) & ~(size_t)3) * 4 + (size_t)rpb * a.C * a.L * 4;
   const dim3 g((unsigned)((long)a.M * a.Kp / rpb)), b(256);
-  if (dt == BF16) hipLaunchKernelGGL(dec_bwd_kernel<bf16raw>, g, b, lds, s, a, rpb);
+  if (dec_mfma(dt, a)) {
+    if (a.N == 256) hipLaunchKernelGGL(dec_bwd_mfma_kernel<16>, dim3(dm_grid(a)), b, 0, s, a);
+    else hipLaunchKernelGGL(dec_bwd_mfma_kernel<32>, dim3(dm_grid(a)), b, 0, s, a);
+  } else if (dt == BF16) hipLaunchKernelGGL(dec_bwd_kernel<bf16raw>, g, b, lds, s, a, rpb);
   else hipLaunchKernelGGL(dec_bwd_kernel<float>, g, b, lds, s, a, rpb);
   return hipGetLastError();
 }

@@ -312,7 +312,9 @@ class DecoderFn(torch.autograd.Function):
 # PIT SI-SNR loss (pit_criterion.py:12-113)
 # ----------------------------------------------------------------------------
 class PITFn(torch.autograd.Function):
-    """(source, est, lengths) -> (loss, max_snr [M,1], est (masked in place), best perm idx)."""
+    """(source, est, lengths) -> (loss, max_snr [M,1], est (masked in place), best perm idx,
+    the reordered estimate [M,C,T] (pit_criterion.py:79-98, written by the same kernel pass
+    that masks est))."""
 
     @staticmethod
     def forward(ctx, source, est, lengths):
@@ -331,21 +333,22 @@ class PITFn(torch.autograd.Function):
         max_snr = torch.empty(M, 1, dtype=torch.float32, device=dev)
         best = torch.empty(M, dtype=torch.int64, device=dev)
         coef = torch.empty(M, C, 4, dtype=torch.float32, device=dev)
+        reordered = torch.empty_like(est)
         nb = lib.ctn_pit_workspace_bytes(ctypes.byref(desc))
         ws = L.workspace(nb, dev)
         L.check(lib.ctn_pit_forward(ctypes.byref(desc), source.data_ptr(), est.data_ptr(), lengths.data_ptr(),
-                                    loss.data_ptr(), max_snr.data_ptr(), best.data_ptr(), None, coef.data_ptr(),
-                                    ws.data_ptr(), nb, L.stream_handle(dev)), "ctn_pit_forward")
+                                    loss.data_ptr(), max_snr.data_ptr(), best.data_ptr(), reordered.data_ptr(),
+                                    coef.data_ptr(), ws.data_ptr(), nb, L.stream_handle(dev)), "ctn_pit_forward")
         ctx.mark_dirty(est)
-        ctx.mark_non_differentiable(best)
+        ctx.mark_non_differentiable(best, reordered)
         # outputs the caller does not differentiate (max_snr, the masked estimate) arrive
         # in backward as None instead of zero-filled tensors
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(source, est, lengths, coef)
-        return loss, max_snr, est, best
+        return loss, max_snr, est, best, reordered
 
     @staticmethod
-    def backward(ctx, g_loss, g_max_snr, g_est_out, _g_best):
+    def backward(ctx, g_loss, g_max_snr, g_est_out, _g_best, _g_reordered):
         lib = L.load()
         source, est, lengths, coef = ctx.saved_tensors
         M, C, T = est.shape

@@ -47,6 +47,18 @@ class _Plan:
         self.chunks = torch.frombuffer(bytearray(bytes(chunks)), dtype=torch.uint8).to(device)
         self.partial = torch.empty(max(n, 1), dtype=torch.float32, device=device)
         self.device = device
+        self._seg_key = None
+        self._seg_dev = None
+
+    def segments(self, segs: list, ptrs: tuple) -> torch.Tensor:
+        """The device segment table for these pointers: uploaded when they change, the
+        previous upload reused when they do not (the steady state: the caching
+        allocator hands the gradients the same blocks every step, and DDP's bucket
+        views never move), so a step issues no host-to-device copy."""
+        if ptrs != self._seg_key:
+            self._seg_dev = upload_segments(segs, self.device)
+            self._seg_key = ptrs
+        return self._seg_dev
 
 
 def upload_segments(segs: list, device) -> torch.Tensor:
@@ -107,7 +119,7 @@ def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0, error_i
     segs = [L.OptSegment(None, g.data_ptr(), None, None, g.numel()) for g in grads]
     key = (dev, tuple((g.numel(), _aligned(g)) for g in grads))
     plan = _cached_plan(_clip_plans, key, lambda: _Plan(segs, dev))
-    segs_dev = upload_segments(segs, dev)
+    segs_dev = plan.segments(segs, tuple(g.data_ptr() for g in grads))
     total = torch.empty((), dtype=torch.float32, device=dev)
     L.check(L.load().ctn_grad_clip_norm(segs_dev.data_ptr(), plan.chunks.data_ptr(), plan.nchunks,
                                         float(max_norm), total.data_ptr(), plan.partial.data_ptr(),
@@ -193,7 +205,7 @@ class Adam(torch.optim.Optimizer):
                         for p, g, m, v in items]
                 key = (dev, tuple((p.numel(), _aligned(p, g, m, v)) for p, g, m, v in items))
                 plan = _cached_plan(self._plans, key, lambda: _Plan(segs, dev))
-                segs_dev = upload_segments(segs, dev)
+                segs_dev = plan.segments(segs, tuple(t.data_ptr() for it in items for t in it))
                 hp = L.AdamHParams(float(group["lr"]), float(b1), float(b2), float(group["eps"]),
                                    float(group["weight_decay"]), n)
                 L.check(lib.ctn_adam_step(segs_dev.data_ptr(), plan.chunks.data_ptr(), plan.nchunks,

@@ -17,23 +17,32 @@ import ctn_lib as L
 import ctn_ops as ops
 
 EPS = 1e-8
+_PERMS = {}
+
+
+def _perms(C, device):
+    """range(C)'s permutations as a device tensor, built once per (C, device): a tensor
+    made from a host list is a synchronous pageable copy, which in the training step
+    stalled the host until the GPU had finished the forward pass."""
+    key = (C, str(device))
+    t = _PERMS.get(key)
+    if t is None:
+        t = torch.tensor(list(permutations(range(C))), dtype=torch.long).to(device)
+        _PERMS[key] = t
+    return t
 
 
 def cal_loss(source, estimate_source, source_lengths):
-    """pit_criterion.py:12-24 -> (loss, max_snr [B,1], estimate_source, reorder_estimate_source)."""
-    loss, max_snr, est, best = ops.PITFn.apply(source, estimate_source, source_lengths)
-    C = source.size(1)
-    perms = source.new_tensor(list(permutations(range(C))), dtype=torch.long)
-    reorder_estimate_source = reorder_source(est.detach(), perms, best)
+    """pit_criterion.py:12-24 -> (loss, max_snr [B,1], estimate_source, reorder_estimate_source).
+    The reordered estimate comes from the loss kernel pass itself (no index_select/gather)."""
+    loss, max_snr, est, _, reorder_estimate_source = ops.PITFn.apply(source, estimate_source, source_lengths)
     return loss, max_snr, est, reorder_estimate_source
 
 
 def cal_si_snr_with_pit(source, estimate_source, source_lengths):
     """pit_criterion.py:27-76 -> (max_snr [B,1], perms [C!,C], max_snr_idx [B])."""
-    _, max_snr, _, best = ops.PITFn.apply(source, estimate_source, source_lengths)
-    C = source.size(1)
-    perms = source.new_tensor(list(permutations(range(C))), dtype=torch.long)
-    return max_snr, perms, best
+    _, max_snr, _, best, _ = ops.PITFn.apply(source, estimate_source, source_lengths)
+    return max_snr, _perms(source.size(1), source.device).clone(), best
 
 
 def reorder_source(source, perms, max_snr_idx):
