@@ -69,6 +69,12 @@ constexpr int WS_FOLD_MAX = 512;   // utterances whose gLN operand stats a workg
 #ifndef CTN_WS_LA8
 #define CTN_WS_LA8 3
 #endif
+#ifndef CTN_WS_STAMP
+#define CTN_WS_STAMP 0
+#endif
+#if CTN_WS_STAMP
+__device__ unsigned long long ws_stamps[256 * 16 * 8];
+#endif
 #ifndef CTN_WS_ORDER
 #define CTN_WS_ORDER 1
 #endif
@@ -498,6 +504,25 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
   // to the last one (never stored).  With SWP the MFMAs of tile t interleave with
   // the epilogue of tile t-1 (two accumulator sets).
   auto clampt = [&](int t) __attribute__((always_inline)) { return t < t1 ? t : t1 - 1; };
+  // Diagnostic build only (tools/microbench/ws_bench.hip -DCTN_WS_STAMP=1): s_memtime
+  // stamps between the loop's phases, per-wave cycle sums in ws_stamps[] (shares only:
+  // the stamps' lgkmcnt(0) forbid overlaps the real kernel has)
+#if CTN_WS_STAMP
+  unsigned long long st_sum[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0;
+#define WS_STAMP(i)                                                                            \
+  do {                                                                                         \
+    __builtin_amdgcn_sched_barrier(0);                                                         \
+    unsigned long long t_;                                                                     \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                 \
+    __builtin_amdgcn_sched_barrier(0);                                                         \
+    if (st_last) st_sum[i] += t_ - st_last;                                                    \
+    st_last = t_;                                                                              \
+  } while (0)
+#else
+#define WS_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
   // LE1 = (alpha <= 1) selects the exact two-instruction PReLU form once per kernel
   auto run = [&](auto le1) __attribute__((always_inline)) {
     if constexpr (!SWP) {
@@ -513,18 +538,26 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
           constexpr int nx = (decltype(u)::value + 1) % PF;   // slot of tile t+1
           const int t = tb + decltype(u)::value;
           if (PF == 1 || t < t1) {
+            WS_STAMP(7);
             lds_barrier();
             if (t > t0) cln_final(t - 1);
+            WS_STAMP(0);
             mfma_tile(sA[t & 1], acc);
             __builtin_amdgcn_sched_barrier(0);
+            WS_STAMP(1);
             if constexpr (CTN_WS_ORDER == 1) {
               // next tile's operand (its buffer's last reader finished before the barrier)
               stage(le1, t + 1, sA[(t + 1) & 1], std::integral_constant<int, nx>{});
+              WS_STAMP(2);
               load_a(clampt(t + 1 + PF), std::integral_constant<int, nx>{});
+              WS_STAMP(3);
               epilogue_math(le1, t, acc);
+              WS_STAMP(4);
               load_r(clampt(t + 1));   // rn(t) consumed above
+              WS_STAMP(5);
               store_out(t);
               store_gh(t + 1);
+              WS_STAMP(6);
             } else {
               epilogue(le1, t, acc);
               load_r(clampt(t + 1));
@@ -579,6 +612,10 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
     lds_barrier();
     cln_final(t1 - 1);
   }
+#if CTN_WS_STAMP
+  if (lane == 0)
+    for (int i = 0; i < 8; ++i) ws_stamps[((size_t)blockIdx.x * 16 + wid) * 8 + i] = st_sum[i];
+#endif
   if constexpr (N1B) {   // fixed-order workgroup sum of the alpha-gradient partials
     const float w = wave_sum_dpp(calpha);
     if (lane == 0) salpha[wid] = w;

@@ -3,6 +3,7 @@
 // build with -DCTN_WS_EXP=<bits> (see ctn_gemm_ws.hip).  Not part of the library.
 #include <stdio.h>
 #include <stdlib.h>
+#include <algorithm>
 #include <vector>
 
 #include "../../conv-tasnet_amd/csrc/ctn_gemm_ws.hip"
@@ -88,6 +89,20 @@ int main() {
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
     const double us = ms * 1e3 / reps;
     printf("EXP=%d  %-24s %8.1f us  %7.0f GB/s (alg)\n", CTN_WS_EXP, c.name, us, c.bytes / (us * 1e-6) / 1e9);
+#if CTN_WS_STAMP
+    {   // per-phase shares of the loop (diagnostic build: read shares, not lengths)
+      std::vector<unsigned long long> h(256 * 16 * 8, 0ull);
+      CK(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(ws_stamps), h.size() * 8));
+      const char* nm[8] = {"barrier", "mfma", "stage", "load_a", "epi_math", "load_r", "stores", "loop"};
+      double sum[8] = {0}, tot = 0;
+      for (size_t w = 0; w < h.size() / 8; ++w)
+        for (int i = 0; i < 8; ++i) sum[i] += (double)h[w * 8 + i];
+      for (int i = 0; i < 8; ++i) tot += sum[i];
+      for (int i = 0; i < 8; ++i) printf("   %-9s %5.1f %%\n", nm[i], 100.0 * sum[i] / tot);
+      std::fill(h.begin(), h.end(), 0ull);
+      CK(hipMemcpyToSymbol(HIP_SYMBOL(ws_stamps), h.data(), h.size() * 8));
+    }
+#endif
   }
   return 0;
 }
