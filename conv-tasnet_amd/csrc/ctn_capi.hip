@@ -931,10 +931,25 @@ extern "C" int ctn_encoder_backward(const ctn_codec_desc* d, const float* mixtur
 // Decoder back: mask conv + nonlinearity + decoder + overlap-add + pad
 // ===========================================================================
 namespace {
+// bf16 MFMA decoder: the basis gradient dV = sum over (frame, speaker) of gframes^T . src
+// runs as a column GEMM (gemm_cols over M*Kp*C rows, P = L padded to 8, Q = N) on
+// operands the decoder backward writes, instead of the LDS-bound frame_outer kernel.
+// CTN_DV_COLS=0 keeps frame_outer (A/B).
+bool dv_cols(const ctn_codec_desc* d) {
+  const char* e = getenv("CTN_DV_COLS");
+  if (e && atoi(e) == 0) return false;
+  return codec_dec_mfma(d->dtype == CTN_DTYPE_BF16 ? BF16 : F32, codec_args(d));
+}
+GemmCols dv_gemm(const ctn_codec_desc* d, int Lp) {
+  GemmCols g{};
+  g.g = Rows{d->M, d->K * d->C, d->Kp * d->C};
+  g.P = Lp; g.Q = d->N;
+  return g;
+}
 struct DecLayout {
-  void *wms, *wmt, *gscore;
-  float *frames, *slabV, *cpartM, *srtmp;
-  int nV, chunksM;
+  void *wms, *wmt, *gscore, *srcb, *gfr;
+  float *frames, *slabV, *cpartM, *cpartV, *srtmp;
+  int nV, chunksM, chunksV, Lp;
   size_t bytes;
 };
 DecLayout dec_layout(const ctn_codec_desc* d, int backward, bool with_mask_conv, void* ws) {
@@ -948,8 +963,16 @@ DecLayout dec_layout(const ctn_codec_desc* d, int backward, bool with_mask_conv,
     L.frames = c.take<float>((size_t)d->M * d->C * d->Kp * d->L * sizeof(float));
   } else {
     CodecArgs a = codec_args(d);
-    L.nV = frame_outer_chunks(a);
-    L.slabV = c.take<float>((size_t)L.nV * d->N * d->L * sizeof(float));
+    if (dv_cols(d)) {
+      L.Lp = (d->L + 7) & ~7;
+      L.srcb = c.take<void>((size_t)rows * d->C * d->N * es);
+      L.gfr = c.take<void>((size_t)rows * d->C * L.Lp * es);
+      L.chunksV = gemm_cols_default_chunks(dv_gemm(d, L.Lp));
+      L.cpartV = c.take<float>((size_t)L.chunksV * L.Lp * d->N * sizeof(float));
+    } else {
+      L.nV = frame_outer_chunks(a);
+      L.slabV = c.take<float>((size_t)L.nV * d->N * d->L * sizeof(float));
+    }
     if (with_mask_conv) {
       L.wmt = c.take<void>((size_t)CN * d->B * es);
       L.gscore = c.take<void>((size_t)rows * CN * es);
@@ -958,7 +981,8 @@ DecLayout dec_layout(const ctn_codec_desc* d, int backward, bool with_mask_conv,
       L.chunksM = gemm_cols_default_chunks(gc);
       L.cpartM = c.take<float>((size_t)L.chunksM * CN * d->B * sizeof(float));
     }
-    L.srtmp = c.take<float>((sr_tmp(L.nV, (long)d->N * d->L) + sr_tmp(L.chunksM, (long)CN * d->B)) * sizeof(float));
+    L.srtmp = c.take<float>((sr_tmp(L.nV > L.chunksV ? L.nV : L.chunksV, (long)d->N * d->L) +
+                             sr_tmp(L.chunksM, (long)CN * d->B)) * sizeof(float));
   }
   L.bytes = c.off + 256;
   return L;
@@ -1023,12 +1047,24 @@ extern "C" int ctn_decoder_backward(const ctn_codec_desc* d, const void* x_last,
   CodecArgs a = codec_args(d);
   a.w_rows = const_cast<void*>(w_rows); a.score = wm ? score : x_last; a.V = V; a.gest = g_est;
   a.gscore = wm ? Ly.gscore : g_x_last; a.gwdec_out = g_w_rows;
+  const bool cols = Ly.srcb != nullptr;
+  if (cols) { a.src_out = Ly.srcb; a.gfr_out = Ly.gfr; a.Lp = Ly.Lp; }
   CTN_HIP(launch_dec_bwd(dt, a, s));
-  CodecArgs fo = a;
-  fo.col_slab = Ly.slabV;
-  CTN_HIP(launch_frame_outer(dt, 1, fo, s));
   SlabBatch sb{};
-  sb.d[sb.nd++] = SlabDesc{Ly.slabV, gV, Ly.nV, d->N * d->L, d->N * d->L};
+  if (cols) {
+    CTN_HIP(launch_dec_gframes(a, s));
+    GemmCols gv = dv_gemm(d, Ly.Lp);
+    gv.A = Ly.gfr; gv.lda = Ly.Lp; gv.B = Ly.srcb; gv.ldb = d->N;
+    gv.Cpart = Ly.cpartV; gv.nchunks = Ly.chunksV;
+    CTN_HIP(launch_gemm_cols(dt, gv, s));
+    // [chunk][Lp][N] partials: the first L rows of each are dV [L][N]
+    sb.d[sb.nd++] = SlabDesc{Ly.cpartV, gV, Ly.chunksV, d->N * d->L, Ly.Lp * d->N};
+  } else {
+    CodecArgs fo = a;
+    fo.col_slab = Ly.slabV;
+    CTN_HIP(launch_frame_outer(dt, 1, fo, s));
+    sb.d[sb.nd++] = SlabDesc{Ly.slabV, gV, Ly.nV, d->N * d->L, d->N * d->L};
+  }
   if (wm) {
     CTN_HIP(launch_prep_weight(dt, wm, CN, d->B, nullptr, Ly.wmt, s));   // [B][CN]
     GemmRows g{};

@@ -23,7 +23,15 @@ struct CodecArgs {
   const float* gest;             // dL/dest [M][C][T]
   void* gscore;                  // dL/dscore rows (backward)
   void* gwdec_out;               // dL/dw from the decoder rows (backward)
+  // bf16 MFMA decoder backward only: the masked sources w * act(score_c) [rows][C][N]
+  // and the frame gradients [rows][C][Lp] (Lp = L rounded up to 8), the two operands
+  // of the decoder basis gradient dV = sum_{r,c} gframes^T src (launch_gemm_cols)
+  void* src_out = nullptr;
+  void* gfr_out = nullptr;
+  int Lp = 0;
 };
+bool codec_dec_mfma(DType dt, const CodecArgs& a);   // the bf16 MFMA decoder applies
+hipError_t launch_dec_gframes(const CodecArgs& a, hipStream_t s);   // gfr_out from gest
 
 hipError_t launch_enc_fwd(DType dt, const CodecArgs& a, hipStream_t s);
 hipError_t launch_enc_bwd_rows(DType dt, const CodecArgs& a, hipStream_t s);

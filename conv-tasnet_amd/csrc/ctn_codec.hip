@@ -596,7 +596,7 @@ __global__ __launch_bounds__(256) void dec_bwd_mfma_kernel(CodecArgs a) {
 #pragma unroll
       for (int c = 0; c < CM; ++c)
         if (c < C) sr[c] = *reinterpret_cast<const v2u*>(sc + r * (long)(C * N) + (long)c * N + n0);
-      float wf[4], gwv[4], go[CM][4];
+      float wf[4], gwv[4], go[CM][4], srcv[CM][4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const uint32_t wd = wr[i >> 1];
@@ -609,6 +609,8 @@ __global__ __launch_bounds__(256) void dec_bwd_mfma_kernel(CodecArgs a) {
           act[c] = s[c];
         }
         dm_act<CM>(a.mask_type, C, act);
+#pragma unroll
+        for (int c = 0; c < CM; ++c) srcv[c][i] = wf[i] * act[c];
         float gwe = 0.f, dot = 0.f, ga[CM];
 #pragma unroll
         for (int c = 0; c < CM; ++c)
@@ -628,12 +630,44 @@ __global__ __launch_bounds__(256) void dec_bwd_mfma_kernel(CodecArgs a) {
           *reinterpret_cast<v2u*>(gsc + r * (long)(C * N) + (long)c * N + n0) =
               v2u{pk_bf16(go[c][0], go[c][1]), pk_bf16(go[c][2], go[c][3])};
       *reinterpret_cast<v2u*>(gw + r * N + n0) = v2u{pk_bf16(gwv[0], gwv[1]), pk_bf16(gwv[2], gwv[3])};
+      if (a.src_out) {
+        bf16raw* so = reinterpret_cast<bf16raw*>(a.src_out);
+#pragma unroll
+        for (int c = 0; c < CM; ++c)
+          if (c < C)
+            *reinterpret_cast<v2u*>(so + r * (long)(C * N) + (long)c * N + n0) =
+                v2u{pk_bf16(srcv[c][0], srcv[c][1]), pk_bf16(srcv[c][2], srcv[c][3])};
+      }
+    }
+  }
+}
+
+// frame gradients gfr[(r, c)][l] = dL/dest[m][c][k*S + l] (0 past K, T or L), bf16, the
+// A operand of the decoder basis gradient; one thread per (row, speaker)
+__global__ __launch_bounds__(256) void dec_gframes_kernel(CodecArgs a) {
+  const long n = (long)a.M * a.Kp * a.C;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int c = (int)(i % a.C);
+    const long r = i / a.C;
+    const int m = (int)(r / a.Kp), k = (int)(r % a.Kp);
+    const float* g = a.gest + ((size_t)m * a.C + c) * a.T + (long)k * a.S;
+    bf16raw* o = reinterpret_cast<bf16raw*>(a.gfr_out) + i * a.Lp;
+    for (int l0 = 0; l0 < a.Lp; l0 += 8) {
+      float f[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int l = l0 + j;
+        f[j] = (k < a.K && l < a.L && (long)k * a.S + l < a.T) ? g[l] : 0.f;
+      }
+      stg16(o + l0, pack_bf16x8v(f));
     }
   }
 }
 
 // CTN_DEC_MFMA=0 keeps the VALU decoder kernels for bf16 too (read per launch: A/B)
-static bool dec_mfma(DType dt, const CodecArgs& a) {
+bool codec_dec_mfma(DType dt, const CodecArgs& a);
+static bool dec_mfma(DType dt, const CodecArgs& a) { return codec_dec_mfma(dt, a); }
+bool codec_dec_mfma(DType dt, const CodecArgs& a) {
   const char* e = getenv("CTN_DEC_MFMA");
   if (e && atoi(e) == 0) return false;
   return dt == BF16 && (a.N == 256 || a.N == 512) && a.L <= 32 && a.C <= 4;
@@ -716,6 +750,14 @@ hipError_t launch_dec_fwd(DType dt, const CodecArgs& a, hipStream_t s) {
   int gb = (int)((total + 255) / 256);
   if (gb > 4096) gb = 4096;
   hipLaunchKernelGGL(ola_fwd_kernel, dim3(gb), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_dec_gframes(const CodecArgs& a, hipStream_t s) {
+  if (!a.gfr_out || a.Lp < a.L || a.Lp % 8) return hipErrorInvalidValue;
+  const long n = (long)a.M * a.Kp * a.C;
+  long g = (n + 255) / 256;
+  hipLaunchKernelGGL(dec_gframes_kernel, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
