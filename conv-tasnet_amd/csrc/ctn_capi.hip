@@ -808,10 +808,24 @@ static CodecArgs codec_args(const ctn_codec_desc* d) {
 }
 
 namespace {
+// bf16: the encoder basis gradient dU[n][l] = sum_r gpre[r][n] x[kS + l] as a column GEMM
+// (gemm_cols, P = N, Q = L padded to 8) of bf16 dL/d(pre-ReLU) rows and mixture frames,
+// instead of the LDS-bound frame_outer kernel.  CTN_DU_COLS=0 keeps frame_outer (A/B).
+bool du_cols(const ctn_codec_desc* d) {
+  const char* e = getenv("CTN_DU_COLS");
+  if (e && atoi(e) == 0) return false;
+  return d->dtype == CTN_DTYPE_BF16 && d->N % 8 == 0;
+}
+GemmCols du_gemm(const ctn_codec_desc* d, int Lp) {
+  GemmCols g{};
+  g.g = Rows{d->M, d->K, d->Kp};
+  g.P = d->N; g.Q = Lp;
+  return g;
+}
 struct EncLayout {
-  void *wbs, *wbt, *gcln;
-  float *gpre, *colE, *slabU, *cpartB, *srtmp;
-  int chunksB, nU, rowblocks;
+  void *wbs, *wbt, *gcln, *gpre_bf, *xfr;
+  float *gpre, *colE, *slabU, *cpartB, *cpartU, *tmpU, *srtmp;
+  int chunksB, nU, rowblocks, chunksU, Lp;
   size_t bytes;
 };
 EncLayout enc_layout(const ctn_codec_desc* d, int backward, void* ws) {
@@ -824,18 +838,27 @@ EncLayout enc_layout(const ctn_codec_desc* d, int backward, void* ws) {
   } else {
     L.wbt = c.take<void>((size_t)d->B * d->N * es);
     L.gcln = c.take<void>((size_t)rows * d->N * es);
-    L.gpre = c.take<float>((size_t)rows * d->N * sizeof(float));
     L.rowblocks = (int)(rows / 128);
     L.colE = c.take<float>((size_t)L.rowblocks * 2 * d->N * sizeof(float));
     CodecArgs a = codec_args(d);
-    L.nU = frame_outer_chunks(a);
-    L.slabU = c.take<float>((size_t)L.nU * d->N * d->L * sizeof(float));
+    if (du_cols(d)) {
+      L.Lp = (d->L + 7) & ~7;
+      L.gpre_bf = c.take<void>((size_t)rows * d->N * 2);
+      L.xfr = c.take<void>((size_t)rows * L.Lp * 2);
+      L.chunksU = gemm_cols_default_chunks(du_gemm(d, L.Lp));
+      L.cpartU = c.take<float>((size_t)L.chunksU * d->N * L.Lp * sizeof(float));
+      L.tmpU = c.take<float>((size_t)d->N * L.Lp * sizeof(float));
+    } else {
+      L.gpre = c.take<float>((size_t)rows * d->N * sizeof(float));
+      L.nU = frame_outer_chunks(a);
+      L.slabU = c.take<float>((size_t)L.nU * d->N * d->L * sizeof(float));
+    }
     GemmCols gc{};
     gc.g = Rows{d->M, d->K, d->Kp}; gc.P = d->B; gc.Q = d->N;
     L.chunksB = gemm_cols_default_chunks(gc);
     L.cpartB = c.take<float>((size_t)L.chunksB * d->B * d->N * sizeof(float));
     const size_t ntmp = sr_tmp(L.chunksB, (long)d->B * d->N) + 2 * sr_tmp(L.rowblocks, d->N) +
-                        sr_tmp(L.nU, (long)d->N * d->L);
+                        sr_tmp(L.nU, (long)d->N * d->L) + sr_tmp(L.chunksU, (long)d->N * L.Lp);
     L.srtmp = c.take<float>(ntmp * sizeof(float));
   }
   L.bytes = c.off + 256;
@@ -896,7 +919,7 @@ extern "C" int ctn_encoder_backward(const ctn_codec_desc* d, const float* mixtur
   CodecArgs a = codec_args(d);
   a.mixture = mixture; a.U = U; a.w_rows = const_cast<void*>(w_rows);
   a.cln_stats = const_cast<float2*>(reinterpret_cast<const float2*>(cln_stats));
-  a.gamma0 = gamma0; a.gwdec = g_w_rows; a.gpre = Ly.gpre;
+  a.gamma0 = gamma0; a.gwdec = g_w_rows; a.gpre = Ly.gpre; a.gpre_bf = Ly.gpre_bf;
   SlabBatch sb{};
   if (g_x0) {
     CTN_HIP(launch_prep_weight(dt, wb, d->B, d->N, nullptr, Ly.wbt, s));   // [N][B]
@@ -919,11 +942,24 @@ extern "C" int ctn_encoder_backward(const ctn_codec_desc* d, const float* mixtur
     sb.d[sb.nd++] = SlabDesc{Ly.colE + d->N, gbeta0, Ly.rowblocks, d->N, 2 * d->N};
   }
   CTN_HIP(launch_enc_bwd_rows(dt, a, s));
-  CodecArgs fo = a;
-  fo.col_slab = Ly.slabU;
-  CTN_HIP(launch_frame_outer(dt, 0, fo, s));
-  sb.d[sb.nd++] = SlabDesc{Ly.slabU, gU, Ly.nU, d->N * d->L, d->N * d->L};
+  const bool cols = Ly.gpre_bf != nullptr;
+  if (cols) {
+    a.Lp = Ly.Lp;
+    CTN_HIP(launch_frames_bf16(a, mixture, 1, Ly.xfr, s));
+    GemmCols gu = du_gemm(d, Ly.Lp);
+    gu.A = Ly.gpre_bf; gu.lda = d->N; gu.B = Ly.xfr; gu.ldb = Ly.Lp;
+    gu.Cpart = Ly.cpartU; gu.nchunks = Ly.chunksU;
+    CTN_HIP(launch_gemm_cols(dt, gu, s));
+    // [chunk][N][Lp] partials -> [N][Lp] -> dU [N][L]
+    sb.d[sb.nd++] = SlabDesc{Ly.cpartU, Ly.Lp == d->L ? gU : Ly.tmpU, Ly.chunksU, d->N * Ly.Lp, d->N * Ly.Lp};
+  } else {
+    CodecArgs fo = a;
+    fo.col_slab = Ly.slabU;
+    CTN_HIP(launch_frame_outer(dt, 0, fo, s));
+    sb.d[sb.nd++] = SlabDesc{Ly.slabU, gU, Ly.nU, d->N * d->L, d->N * d->L};
+  }
   CTN_HIP(launch_slab_reduce(sb, Ly.srtmp, s));
+  if (cols && Ly.Lp != d->L) CTN_HIP(launch_unpad_cols(Ly.tmpU, d->N, Ly.Lp, d->L, gU, s));
   return CTN_OK;
 }
 

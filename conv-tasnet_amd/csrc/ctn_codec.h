@@ -29,9 +29,17 @@ struct CodecArgs {
   void* src_out = nullptr;
   void* gfr_out = nullptr;
   int Lp = 0;
+  // bf16 encoder backward on the column GEMM: dL/d(pre-ReLU) rows in bf16 (instead of
+  // the fp32 gpre), the operand of dU = gpre^T . mixture frames
+  void* gpre_bf = nullptr;
 };
 bool codec_dec_mfma(DType dt, const CodecArgs& a);   // the bf16 MFMA decoder applies
 hipError_t launch_dec_gframes(const CodecArgs& a, hipStream_t s);   // gfr_out from gest
+// bf16 frames [M*Kp*C][Lp] of a signal [M][C][T] (frame k = samples k*S .. k*S+L-1,
+// zero past K, T and L): dec_gframes on gest, and the mixture frames of the encoder
+hipError_t launch_frames_bf16(const CodecArgs& a, const float* sig, int C, void* out, hipStream_t s);
+// out[n][l] = tmp[n][l] for l < L, tmp [N][Lp]
+hipError_t launch_unpad_cols(const float* tmp, int N, int Lp, int L, float* out, hipStream_t s);
 
 hipError_t launch_enc_fwd(DType dt, const CodecArgs& a, hipStream_t s);
 hipError_t launch_enc_bwd_rows(DType dt, const CodecArgs& a, hipStream_t s);

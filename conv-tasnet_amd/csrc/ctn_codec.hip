@@ -140,7 +140,8 @@ __global__ __launch_bounds__(256) void enc_bwd_rows_kernel(CodecArgs a) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) out[e] = wv[e] > 0.f ? gd[e] : 0.f;   // ReLU backward
       }
-      Vec8<float>::store(a.gpre + (size_t)r * N + c * 8, out);
+      if (a.gpre_bf) Vec8<bf16raw>::store(reinterpret_cast<bf16raw*>(a.gpre_bf) + (size_t)r * N + c * 8, out);
+      else Vec8<float>::store(a.gpre + (size_t)r * N + c * 8, out);
     }
   }
   if (a.col_slab) {
@@ -642,16 +643,17 @@ __global__ __launch_bounds__(256) void dec_bwd_mfma_kernel(CodecArgs a) {
   }
 }
 
-// frame gradients gfr[(r, c)][l] = dL/dest[m][c][k*S + l] (0 past K, T or L), bf16, the
-// A operand of the decoder basis gradient; one thread per (row, speaker)
-__global__ __launch_bounds__(256) void dec_gframes_kernel(CodecArgs a) {
-  const long n = (long)a.M * a.Kp * a.C;
+// frames of a signal sig [M][C][T] as bf16 rows fr[(r, c)][l] = sig[m][c][k*S + l] (0 past
+// K, T or L): the frame gradients of the decoder basis gradient (sig = dL/dest) and the
+// mixture frames of the encoder's (C = 1); one thread per (row, channel)
+__global__ __launch_bounds__(256) void frames_bf16_kernel(CodecArgs a, const float* sig, int C, bf16raw* out) {
+  const long n = (long)a.M * a.Kp * C;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
-    const int c = (int)(i % a.C);
-    const long r = i / a.C;
+    const int c = (int)(i % C);
+    const long r = i / C;
     const int m = (int)(r / a.Kp), k = (int)(r % a.Kp);
-    const float* g = a.gest + ((size_t)m * a.C + c) * a.T + (long)k * a.S;
-    bf16raw* o = reinterpret_cast<bf16raw*>(a.gfr_out) + i * a.Lp;
+    const float* g = sig + ((size_t)m * C + c) * a.T + (long)k * a.S;
+    bf16raw* o = out + i * a.Lp;
     for (int l0 = 0; l0 < a.Lp; l0 += 8) {
       float f[8];
 #pragma unroll
@@ -753,11 +755,24 @@ hipError_t launch_dec_fwd(DType dt, const CodecArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_dec_gframes(const CodecArgs& a, hipStream_t s) {
-  if (!a.gfr_out || a.Lp < a.L || a.Lp % 8) return hipErrorInvalidValue;
-  const long n = (long)a.M * a.Kp * a.C;
+hipError_t launch_frames_bf16(const CodecArgs& a, const float* sig, int C, void* out, hipStream_t s) {
+  if (!out || !sig || a.Lp < a.L || a.Lp % 8 || C < 1) return hipErrorInvalidValue;
+  const long n = (long)a.M * a.Kp * C;
   long g = (n + 255) / 256;
-  hipLaunchKernelGGL(dec_gframes_kernel, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(frames_bf16_kernel, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, s, a, sig, C,
+                     reinterpret_cast<bf16raw*>(out));
+  return hipGetLastError();
+}
+hipError_t launch_dec_gframes(const CodecArgs& a, hipStream_t s) {
+  return launch_frames_bf16(a, a.gest, a.C, a.gfr_out, s);
+}
+
+__global__ __launch_bounds__(256) void unpad_cols_kernel(const float* tmp, int N, int Lp, int L, float* out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < N * L) out[i] = tmp[(i / L) * Lp + i % L];
+}
+hipError_t launch_unpad_cols(const float* tmp, int N, int Lp, int L, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(unpad_cols_kernel, dim3((N * L + 255) / 256), dim3(256), 0, s, tmp, N, Lp, L, out);
   return hipGetLastError();
 }
 

@@ -1,5 +1,6 @@
 """bf16 decoder on the matrix cores (ctn_codec.hip dec_fwd_mfma / dec_bwd_mfma, used for
-N in {256, 512}) against the VALU decoder kernels (CTN_DEC_MFMA=0, the same bf16
+N in {256, 512}; the decoder and encoder basis gradients as column GEMMs) against the
+VALU decoder kernels and frame_outer (CTN_DEC_MFMA=0, CTN_DU_COLS=0, the same bf16
 inputs) and against fp32 mode, through the whole model forward and backward so the mask
 conv, nonlinearity, basis, overlap-add and their gradients are all on the path
 (conv_tasnet.py:128-140, utils.py:9-46).  The MFMA path rounds the masked source and the
@@ -20,7 +21,10 @@ def rel(a, b):
 
 
 def _run(model, mix, G, mfma, monkeypatch):
+    # the matrix-core paths together: the MFMA decoder (with dV as a column GEMM) and the
+    # encoder's dU as a column GEMM; off = the VALU decoder and frame_outer for both
     monkeypatch.setenv("CTN_DEC_MFMA", "1" if mfma else "0")
+    monkeypatch.setenv("CTN_DU_COLS", "1" if mfma else "0")
     model.zero_grad(set_to_none=True)
     est = model(mix)
     (est * G).sum().backward()
