@@ -718,6 +718,7 @@ struct SrJob {
   const float* src;
   float* dst;
   int nparts, n, pstride, nslices;
+  int vec4;   // 4 consecutive outputs per lane (16-byte loads); same per-output order
 };
 struct SrBatch {
   SrJob j[16];
@@ -726,12 +727,57 @@ struct SrBatch {
 
 __global__ __launch_bounds__(256) void slab_reduce_kernel(SrBatch b) {
   __shared__ double part[4][64];
+  __shared__ double part4[4][4][64];
   const SrJob d = b.j[blockIdx.z];
   if ((int)blockIdx.y >= d.nslices) return;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int q0 = blockIdx.y * SR_SLICE;
   const int q1 = d.nslices == 1 ? d.nparts : (q0 + SR_SLICE < d.nparts ? q0 + SR_SLICE : d.nparts);
   float* out = d.nslices > 1 ? d.dst + (size_t)blockIdx.y * d.n : d.dst;
+  if (d.vec4) {   // lanes own 4 consecutive outputs: 1 KiB per wave load instead of 256 B
+    for (int i0 = blockIdx.x * 256; i0 < d.n; i0 += gridDim.x * 256) {
+      const int i = i0 + 4 * lane;
+      double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+      if (i < d.n) {
+        const float* src = d.src + i;
+        int q = q0 + w;
+        for (; q + 28 < q1; q += 32) {
+          float4 v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(src + (size_t)(q + 4 * u) * d.pstride);
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            a0 += (double)v[u].x;
+            a1 += (double)v[u].y;
+            a2 += (double)v[u].z;
+            a3 += (double)v[u].w;
+          }
+        }
+        for (; q < q1; q += 4) {
+          const float4 v = *reinterpret_cast<const float4*>(src + (size_t)q * d.pstride);
+          a0 += (double)v.x;
+          a1 += (double)v.y;
+          a2 += (double)v.z;
+          a3 += (double)v.w;
+        }
+      }
+      part4[w][0][lane] = a0;
+      part4[w][1][lane] = a1;
+      part4[w][2][lane] = a2;
+      part4[w][3][lane] = a3;
+      __syncthreads();
+      if (w == 0 && i < d.n) {
+        float4 o;
+        o.x = (float)(((part4[0][0][lane] + part4[1][0][lane]) + part4[2][0][lane]) + part4[3][0][lane]);
+        o.y = (float)(((part4[0][1][lane] + part4[1][1][lane]) + part4[2][1][lane]) + part4[3][1][lane]);
+        o.z = (float)(((part4[0][2][lane] + part4[1][2][lane]) + part4[2][2][lane]) + part4[3][2][lane]);
+        o.w = (float)(((part4[0][3][lane] + part4[1][3][lane]) + part4[2][3][lane]) + part4[3][3][lane]);
+        *reinterpret_cast<float4*>(out + i) = o;
+      }
+      __syncthreads();
+    }
+    return;
+  }
   for (int i0 = blockIdx.x * 64; i0 < d.n; i0 += gridDim.x * 64) {
     const int i = i0 + lane;
     double acc = 0.0;
@@ -756,12 +802,13 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(SrBatch b) {
 
 static hipError_t sr_launch(const SrBatch& b, hipStream_t s) {
   if (b.nj <= 0) return hipSuccess;
-  int mx = 1, ms = 1;
+  int gx = 1, ms = 1;
   for (int i = 0; i < b.nj; ++i) {
-    mx = b.j[i].n > mx ? b.j[i].n : mx;
+    const int per = b.j[i].vec4 ? 256 : 64;
+    const int g = (b.j[i].n + per - 1) / per;
+    gx = g > gx ? g : gx;
     ms = b.j[i].nslices > ms ? b.j[i].nslices : ms;
   }
-  int gx = (mx + 63) / 64;
   if (gx > 1024) gx = 1024;
   hipLaunchKernelGGL(slab_reduce_kernel, dim3(gx, ms, b.nj), dim3(256), 0, s, b);
   return hipGetLastError();
@@ -780,17 +827,20 @@ hipError_t launch_slab_reduce(const SlabBatch& b, float* tmp, hipStream_t s) {
   if (b.nd <= 0) return hipSuccess;
   SrBatch p1{}, p2{};
   size_t off = 0;
+  auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
   for (int i = 0; i < b.nd; ++i) {
     const SlabDesc& d = b.d[i];
     const int ns = (d.nparts + SR_SLICE - 1) / SR_SLICE;
+    const bool v4 = d.n % 4 == 0 && d.pstride % 4 == 0 && a16(d.src) && a16(d.dst);
     if (ns <= 1 || !tmp) {
       // single pass straight into dst (also the fallback when no scratch is given)
-      p2.j[p2.nj++] = SrJob{d.src, d.dst, d.nparts, d.n, d.pstride, 1};
+      p2.j[p2.nj++] = SrJob{d.src, d.dst, d.nparts, d.n, d.pstride, 1, v4 ? 1 : 0};
     } else {
       float* t = tmp + off;
       off += (size_t)ns * d.n;
-      p1.j[p1.nj++] = SrJob{d.src, t, d.nparts, d.n, d.pstride, ns};
-      p2.j[p2.nj++] = SrJob{t, d.dst, ns, d.n, d.n, 1};
+      const bool v4t = v4 && a16(t);
+      p1.j[p1.nj++] = SrJob{d.src, t, d.nparts, d.n, d.pstride, ns, v4t ? 1 : 0};
+      p2.j[p2.nj++] = SrJob{t, d.dst, ns, d.n, d.n, 1, v4t ? 1 : 0};
     }
   }
   hipError_t e = sr_launch(p1, s);
