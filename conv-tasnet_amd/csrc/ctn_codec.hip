@@ -534,10 +534,13 @@ __global__ __launch_bounds__(256) void dec_fwd_mfma_kernel(CodecArgs a) {
   }
 }
 
-template <int NBN>   // N / 16
+template <int NBN, int CM>   // N / 16, speakers (compile time: per-speaker arrays stay in registers)
 __global__ __launch_bounds__(256) void dec_bwd_mfma_kernel(CodecArgs a) {
-  constexpr int N = NBN * 16, CM = 4;
+  constexpr int N = NBN * 16;
+  static_assert(NBN % 2 == 0, "two channel blocks per round");
   __shared__ v4u afrag[NBN * 64];
+  constexpr int TS = 36;   // tile row stride (floats): 32 channels + 4 of padding against bank conflicts
+  __shared__ __attribute__((aligned(16))) float gtile[DM_WAVES * CM * 16 * TS];   // per-wave transpose tiles
   const int lane = threadIdx.x & 63, lr = lane & 15, lg = lane >> 4, wv = threadIdx.x >> 6;
   const int L = a.L, C = a.C, S = a.S, K = a.K, Kp = a.Kp;
   // basis fragments (A operand) [nb][lane]: row n = nb*16 + (lane & 15), k = l =
@@ -580,33 +583,45 @@ __global__ __launch_bounds__(256) void dec_bwd_mfma_kernel(CodecArgs a) {
         gb[c] = pack_bf16x8v(f);
       }
     }
-#pragma unroll 2
-    for (int nb = 0; nb < NBN; ++nb) {
-      // gsrc_c[row r0 + lr][n = nb*16 + 4lg + i]
-      f32x4_t gs[CM];
+    // Two 16-channel blocks per round: the MFMA leaves lane (n = 4lg + i, r = lr); the
+    // products go through this wave's LDS tile [16 rows][32 channels (+4 pad)] so that each lane
+    // then owns 8 consecutive channels of one row (r = lane / 4, n = 8 * (lane % 4)) and
+    // every load and store below is 16 bytes (64-byte row segments).
+    float* tile = gtile + wv * (CM * 16 * TS);
+    const int er = lane >> 2, en = 8 * (lane & 3);   // element-wise row / first channel in the round
+#pragma unroll 1
+    for (int nb = 0; nb < NBN; nb += 2) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int c = 0; c < CM; ++c)
+          if (c < C) {
+            const f32x4_t g = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8_t, afrag[(nb + h) * 64 + lane]), __builtin_bit_cast(bf16x8_t, gb[c]),
+                f32x4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            *reinterpret_cast<float4*>(tile + (c * 16 + lr) * TS + h * 16 + 4 * lg) = float4{g[0], g[1], g[2], g[3]};
+          }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the wave's own tile: no barrier needed
+      const long r = r0 + er;
+      const int n0 = nb * 16 + en;
+      float wf[8], sv[CM][8], gs[CM][8];
+      unpack_bf16x8(ldg16(w + r * N + n0), wf);
 #pragma unroll
       for (int c = 0; c < CM; ++c)
-        if (c < C)
-          gs[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, afrag[nb * 64 + lane]),
-                                                        __builtin_bit_cast(bf16x8_t, gb[c]),
-                                                        f32x4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-      const long r = r0 + lr;
-      const int n0 = nb * 16 + 4 * lg;
-      const v2u wr = *reinterpret_cast<const v2u*>(w + r * N + n0);
-      v2u sr[CM];
+        if (c < C) {
+          unpack_bf16x8(ldg16(sc + r * (long)(C * N) + (long)c * N + n0), sv[c]);
+          const float4 g0 = *reinterpret_cast<const float4*>(tile + (c * 16 + er) * TS + en);
+          const float4 g1 = *reinterpret_cast<const float4*>(tile + (c * 16 + er) * TS + en + 4);
+          gs[c][0] = g0.x; gs[c][1] = g0.y; gs[c][2] = g0.z; gs[c][3] = g0.w;
+          gs[c][4] = g1.x; gs[c][5] = g1.y; gs[c][6] = g1.z; gs[c][7] = g1.w;
+        }
+      float gwv[8], go[CM][8], srcv[CM][8];
 #pragma unroll
-      for (int c = 0; c < CM; ++c)
-        if (c < C) sr[c] = *reinterpret_cast<const v2u*>(sc + r * (long)(C * N) + (long)c * N + n0);
-      float wf[4], gwv[4], go[CM][4], srcv[CM][4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint32_t wd = wr[i >> 1];
-        wf[i] = __uint_as_float((i & 1) ? (wd & 0xffff0000u) : (wd << 16));
+      for (int i = 0; i < 8; ++i) {
         float s[CM], act[CM];
 #pragma unroll
         for (int c = 0; c < CM; ++c) {
-          const uint32_t sd = c < C ? sr[c][i >> 1] : 0u;
-          s[c] = __uint_as_float((i & 1) ? (sd & 0xffff0000u) : (sd << 16));
+          s[c] = c < C ? sv[c][i] : 0.f;
           act[c] = s[c];
         }
         dm_act<CM>(a.mask_type, C, act);
@@ -627,18 +642,15 @@ __global__ __launch_bounds__(256) void dec_bwd_mfma_kernel(CodecArgs a) {
       }
 #pragma unroll
       for (int c = 0; c < CM; ++c)
-        if (c < C)
-          *reinterpret_cast<v2u*>(gsc + r * (long)(C * N) + (long)c * N + n0) =
-              v2u{pk_bf16(go[c][0], go[c][1]), pk_bf16(go[c][2], go[c][3])};
-      *reinterpret_cast<v2u*>(gw + r * N + n0) = v2u{pk_bf16(gwv[0], gwv[1]), pk_bf16(gwv[2], gwv[3])};
+        if (c < C) stg16(gsc + r * (long)(C * N) + (long)c * N + n0, pack_bf16x8v(go[c]));
+      stg16(gw + r * N + n0, pack_bf16x8v(gwv));
       if (a.src_out) {
         bf16raw* so = reinterpret_cast<bf16raw*>(a.src_out);
 #pragma unroll
         for (int c = 0; c < CM; ++c)
-          if (c < C)
-            *reinterpret_cast<v2u*>(so + r * (long)(C * N) + (long)c * N + n0) =
-                v2u{pk_bf16(srcv[c][0], srcv[c][1]), pk_bf16(srcv[c][2], srcv[c][3])};
+          if (c < C) stg16(so + r * (long)(C * N) + (long)c * N + n0, pack_bf16x8v(srcv[c]));
       }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // tile reads done before the next round's writes
     }
   }
 }
@@ -782,8 +794,15 @@ hipError_t launch_dec_bwd(DType dt, const CodecArgs& a, hipStream_t s) {
   const size_t lds = (((size_t)a.N * a.L + 3) & ~(size_t)3) * 4 + (size_t)rpb * a.C * a.L * 4;
   const dim3 g((unsigned)((long)a.M * a.Kp / rpb)), b(256);
   if (dec_mfma(dt, a)) {
-    if (a.N == 256) hipLaunchKernelGGL(dec_bwd_mfma_kernel<16>, dim3(dm_grid(a)), b, 0, s, a);
-    else hipLaunchKernelGGL(dec_bwd_mfma_kernel<32>, dim3(dm_grid(a)), b, 0, s, a);
+#define CTN_DBM(NBN_)                                                                                     \
+    switch (a.C) {                                                                                      \
+      case 1: hipLaunchKernelGGL((dec_bwd_mfma_kernel<NBN_, 1>), dim3(dm_grid(a)), b, 0, s, a); break;  \
+      case 2: hipLaunchKernelGGL((dec_bwd_mfma_kernel<NBN_, 2>), dim3(dm_grid(a)), b, 0, s, a); break;  \
+      case 3: hipLaunchKernelGGL((dec_bwd_mfma_kernel<NBN_, 3>), dim3(dm_grid(a)), b, 0, s, a); break;  \
+      default: hipLaunchKernelGGL((dec_bwd_mfma_kernel<NBN_, 4>), dim3(dm_grid(a)), b, 0, s, a); break; \
+    }
+    if (a.N == 256) { CTN_DBM(16) } else { CTN_DBM(32) }
+#undef CTN_DBM
   } else if (dt == BF16) hipLaunchKernelGGL(dec_bwd_kernel<bf16raw>, g, b, lds, s, a, rpb);
   else hipLaunchKernelGGL(dec_bwd_kernel<float>, g, b, lds, s, a, rpb);
   return hipGetLastError();
