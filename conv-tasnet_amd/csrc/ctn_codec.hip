@@ -465,9 +465,9 @@ template <int CM> CTN_DEV void dm_act(int mask_type, int C, float (&x)[CM]) {
   }
 }
 
-template <int KBN>
+template <int KBN, int CM>   // N / 32, speakers
 __global__ __launch_bounds__(256) void dec_fwd_mfma_kernel(CodecArgs a) {
-  constexpr int N = KBN * 32, CM = 4;
+  constexpr int N = KBN * 32;
   __shared__ v4u bfrag[2 * KBN * 64];
   const int lane = threadIdx.x & 63, lg = lane >> 4, wv = threadIdx.x >> 6;
   const int L = a.L, C = a.C, K = a.K, Kp = a.Kp;
@@ -678,6 +678,90 @@ __global__ __launch_bounds__(256) void frames_bf16_kernel(CodecArgs a, const flo
   }
 }
 
+// bf16-storage encoder forward on the fp32 matrix cores (N = 16*NBN, L <= 32):
+// w^T[n][r] = ReLU(sum_l U[n][l] x[kS+l]) with v_mfma_f32_16x16x4_f32 (exact fp32 operands,
+// as the VALU kernel), U as A operands in LDS and the mixture frames as B operands (one
+// sample per lane and k-step); the products go through a per-wave LDS tile as in
+// dec_bwd_mfma so each lane stores 8 consecutive channels of one frame (16 bytes) and
+// keeps them for the frame's cLN statistics (two-pass over the values the four lanes of
+// the frame hold, reduced with DPP quad permutes): enc_fwd_kernel's arithmetic, fp32.
+template <int NBN>
+__global__ __launch_bounds__(256) void enc_fwd_mfma_kernel(CodecArgs a) {
+  constexpr int N = NBN * 16, NR = NBN / 2;   // rounds of 32 channels
+  constexpr int TS = 36, KKM = 8;              // k-steps of 4 samples: L <= 32
+  __shared__ float afr[NBN * KKM * 64];         // [nb][kk][lane] = U[nb*16 + lane%16][4kk + lane/16]
+  __shared__ __attribute__((aligned(16))) float tiles[DM_WAVES * 16 * TS];
+  const int lane = threadIdx.x & 63, lr = lane & 15, lg = lane >> 4, wv = threadIdx.x >> 6;
+  const int L = a.L, S = a.S, K = a.K, Kp = a.Kp, KK = (L + 3) / 4;
+  for (int i = threadIdx.x; i < NBN * KKM * 64; i += 256) {
+    const int ln = i & 63, kk = (i >> 6) % KKM, nb = i / (64 * KKM), l = 4 * kk + (ln >> 4);
+    afr[i] = l < L ? a.U[(size_t)(nb * 16 + (ln & 15)) * L + l] : 0.f;
+  }
+  __syncthreads();
+  bf16raw* w = reinterpret_cast<bf16raw*>(a.w_rows);
+  float* tile = tiles + wv * 16 * TS;
+  const int er = lane >> 2, en = 8 * (lane & 3);
+  const long nblk = (long)a.M * Kp / 16;
+  for (long blk = (long)blockIdx.x * DM_WAVES + wv; blk < nblk; blk += (long)gridDim.x * DM_WAVES) {
+    const long r0 = blk * 16;
+    const int m = (int)(r0 / Kp), k0 = (int)(r0 - (long)m * Kp);
+    float fb[KKM];   // frames (B operand): column r = lr, sample l = 4kk + lg
+    {
+      const int k = k0 + lr;
+      const float* x = a.mixture + (size_t)m * a.T + (long)k * S;
+#pragma unroll
+      for (int kk = 0; kk < KKM; ++kk) {
+        const int l = 4 * kk + lg;
+        fb[kk] = (kk < KK && k < K && l < L && (long)k * S + l < a.T) ? x[l] : 0.f;
+      }
+    }
+    const int k = k0 + er;
+    const bool valid = k < K;
+    float v[NR][8];
+#pragma unroll
+    for (int rd = 0; rd < NR; ++rd) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        f32x4_t g = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < KKM; ++kk)
+          if (kk < KK) g = __builtin_amdgcn_mfma_f32_16x16x4f32(afr[((2 * rd + h) * KKM + kk) * 64 + lane], fb[kk], g, 0, 0, 0);
+        *reinterpret_cast<float4*>(tile + lr * TS + h * 16 + 4 * lg) = float4{g[0], g[1], g[2], g[3]};
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const float4 g0 = *reinterpret_cast<const float4*>(tile + er * TS + en);
+      const float4 g1 = *reinterpret_cast<const float4*>(tile + er * TS + en + 4);
+      const float t[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[rd][e] = valid ? (t[e] > 0.f ? t[e] : 0.f) : 0.f;
+      stg16(w + (size_t)(r0 + er) * N + rd * 32 + en, pack_bf16x8v(v[rd]));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    if (a.cln_stats) {
+      // the frame's 256 values are spread over its 4 lanes (quad): quad sums by DPP
+      float sm = 0.f;
+#pragma unroll
+      for (int rd = 0; rd < NR; ++rd)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sm += v[rd][e];
+      sm += dpp_f<0xB1, 0xF>(sm);   // quad_perm [1,0,3,2]
+      sm += dpp_f<0x4E, 0xF>(sm);   // quad_perm [2,3,0,1]
+      const float mean = sm / (float)N;
+      float q = 0.f;
+#pragma unroll
+      for (int rd = 0; rd < NR; ++rd)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) q += (v[rd][e] - mean) * (v[rd][e] - mean);
+      q += dpp_f<0xB1, 0xF>(q);
+      q += dpp_f<0x4E, 0xF>(q);
+      if ((lane & 3) == 0) {
+        const float rstd = 1.0f / sqrtf(q / (float)N + 1e-8f);
+        a.cln_stats[r0 + er] = valid ? make_float2(mean, rstd) : make_float2(0.f, 1.f);
+      }
+    }
+  }
+}
+
 // CTN_DEC_MFMA=0 keeps the VALU decoder kernels for bf16 too (read per launch: A/B)
 bool codec_dec_mfma(DType dt, const CodecArgs& a);
 static bool dec_mfma(DType dt, const CodecArgs& a) { return codec_dec_mfma(dt, a); }
@@ -704,7 +788,11 @@ hipError_t launch_enc_fwd(DType dt, const CodecArgs& a, hipStream_t s) {
   if (!codec_ok(a)) return hipErrorInvalidValue;
   const size_t lds = ((size_t)a.L * a.N + (EN_RPB - 1) * a.S + a.L) * sizeof(float);
   const dim3 g((unsigned)((long)a.M * a.Kp / EN_RPB)), b(256);
-  if (dt == BF16) hipLaunchKernelGGL(enc_fwd_kernel<bf16raw>, g, b, lds, s, a);
+  const char* e = getenv("CTN_ENC_MFMA");
+  const bool mf = dt == BF16 && (!e || atoi(e) != 0) && (a.N == 256 || a.N == 512) && a.L <= 32;
+  if (mf && a.N == 256) hipLaunchKernelGGL(enc_fwd_mfma_kernel<16>, dim3(dm_grid(a)), b, 0, s, a);
+  else if (mf) hipLaunchKernelGGL(enc_fwd_mfma_kernel<32>, dim3(dm_grid(a)), b, 0, s, a);
+  else if (dt == BF16) hipLaunchKernelGGL(enc_fwd_kernel<bf16raw>, g, b, lds, s, a);
   else hipLaunchKernelGGL(enc_fwd_kernel<float>, g, b, lds, s, a);
   return hipGetLastError();
 }
@@ -754,8 +842,15 @@ hipError_t launch_dec_fwd(DType dt, const CodecArgs& a, hipStream_t s) {
   const size_t lds = (((size_t)a.N * a.L + 3) & ~(size_t)3) * 4 + (size_t)rpb * a.C * a.N * 4;
   const dim3 g((unsigned)((long)a.M * a.Kp / rpb)), b(256);
   if (dec_mfma(dt, a)) {
-    if (a.N == 256) hipLaunchKernelGGL(dec_fwd_mfma_kernel<8>, dim3(dm_grid(a)), b, 0, s, a);
-    else hipLaunchKernelGGL(dec_fwd_mfma_kernel<16>, dim3(dm_grid(a)), b, 0, s, a);
+#define CTN_DFM(KBN_)                                                                                    \
+    switch (a.C) {                                                                                     \
+      case 1: hipLaunchKernelGGL((dec_fwd_mfma_kernel<KBN_, 1>), dim3(dm_grid(a)), b, 0, s, a); break; \
+      case 2: hipLaunchKernelGGL((dec_fwd_mfma_kernel<KBN_, 2>), dim3(dm_grid(a)), b, 0, s, a); break; \
+      case 3: hipLaunchKernelGGL((dec_fwd_mfma_kernel<KBN_, 3>), dim3(dm_grid(a)), b, 0, s, a); break; \
+      default: hipLaunchKernelGGL((dec_fwd_mfma_kernel<KBN_, 4>), dim3(dm_grid(a)), b, 0, s, a); break; \
+    }
+    if (a.N == 256) { CTN_DFM(8) } else { CTN_DFM(16) }
+#undef CTN_DFM
   } else if (dt == BF16) hipLaunchKernelGGL(dec_fwd_kernel<bf16raw>, g, b, lds, s, a, rpb);
   else hipLaunchKernelGGL(dec_fwd_kernel<float>, g, b, lds, s, a, rpb);
   hipError_t e = hipGetLastError();
