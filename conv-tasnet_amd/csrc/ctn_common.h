@@ -86,6 +86,65 @@ CTN_DEV void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// Buffer resources and LDS-DMA (the dual GEMM and the plain column GEMM)
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+CTN_DEV rsrc_t du_rsrc(const void* p, long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL),
+                                           0x00020000);
+}
+// LDS-DMA (buffer_load ... lds) of one 16-byte (4-byte) piece per lane into the LDS
+// block at the wave-uniform byte address `lds` (lane l lands at lds + 16 l).  Written
+// as inline asm so that the compiler does not see an LDS write it cannot place: it
+// would put a vmcnt(0) in front of every later LDS read it cannot prove disjoint,
+// draining the ring.  The kernel counts these loads itself (du_vmwait).
+CTN_DEV uint32_t du_ldsaddr(const char* p) {
+  return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)p);
+}
+CTN_DEV void du_dma16(rsrc_t r, const char* lds, uint32_t voff, int soff) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(r), "s"(du_ldsaddr(lds)), "s"(soff)
+               : "memory");
+}
+CTN_DEV void du_dma4(rsrc_t r, const char* lds, uint32_t voff, int soff) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(r), "s"(du_ldsaddr(lds)), "s"(soff)
+               : "memory");
+}
+// s_waitcnt vmcnt(n) for a wave-uniform n (clamped down: waiting for more is safe)
+CTN_DEV void du_vmwait(int n) {
+  switch (n < 0 ? 0 : n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+  }
+}
+// the same up to vmcnt(23) (the WS GEMM's ring)
+CTN_DEV void vmwait23(int n) {
+#define CTN_VMW(k) \
+  case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+  switch (n < 0 ? 0 : n) {
+    CTN_VMW(0) CTN_VMW(1) CTN_VMW(2) CTN_VMW(3) CTN_VMW(4) CTN_VMW(5) CTN_VMW(6) CTN_VMW(7)
+    CTN_VMW(8) CTN_VMW(9) CTN_VMW(10) CTN_VMW(11) CTN_VMW(12) CTN_VMW(13) CTN_VMW(14) CTN_VMW(15)
+    CTN_VMW(16) CTN_VMW(17) CTN_VMW(18) CTN_VMW(19) CTN_VMW(20) CTN_VMW(21) CTN_VMW(22)
+    default: asm volatile("s_waitcnt vmcnt(23)" ::: "memory"); break;
+  }
+#undef CTN_VMW
+}
+
 // 8 bf16 held in a 16-byte register value <-> 8 floats (no memory round trip)
 CTN_DEV void unpack_bf16x8(const u128& v, float f[8]) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};

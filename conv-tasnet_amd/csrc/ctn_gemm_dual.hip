@@ -78,11 +78,6 @@ CTN_DEV s16x4_t du_tr(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(p));
 }
 
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
-CTN_DEV rsrc_t du_rsrc(const void* p, long bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL),
-                                           0x00020000);
-}
 constexpr uint32_t DU_OOB = 0x80000000u;   // voffset past every buffer: loads return 0
 
 // NV consecutive bf16 (NV = 4: 8-byte access, NV = 8: 16-byte access) through a buffer resource
@@ -112,47 +107,6 @@ template <int NV> CTN_DEV void du_bstore(rsrc_t r, uint32_t voff, int soff, cons
     typedef uint32_t v2u __attribute__((ext_vector_type(2)));
     const v2u o = {pk_bf16(v[0][0], v[0][1]), pk_bf16(v[1][0], v[1][1])};
     __builtin_amdgcn_raw_buffer_store_b64(o, r, voff, soff, 0);
-  }
-}
-
-// LDS-DMA (buffer_load ... lds) of one 16-byte (4-byte) piece per lane into the LDS
-// block at the wave-uniform byte address `lds` (lane l lands at lds + 16 l).  Written
-// as inline asm so that the compiler does not see an LDS write it cannot place: it
-// would put a vmcnt(0) in front of every later LDS read it cannot prove disjoint,
-// draining the ring.  The kernel counts these loads itself (du_vmwait).
-CTN_DEV uint32_t du_ldsaddr(const char* p) {
-  return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)p);
-}
-CTN_DEV void du_dma16(rsrc_t r, const char* lds, uint32_t voff, int soff) {
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(voff), "s"(r), "s"(du_ldsaddr(lds)), "s"(soff)
-               : "memory");
-}
-CTN_DEV void du_dma4(rsrc_t r, const char* lds, uint32_t voff, int soff) {
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(voff), "s"(r), "s"(du_ldsaddr(lds)), "s"(soff)
-               : "memory");
-}
-// s_waitcnt vmcnt(n) for a wave-uniform n (clamped down: waiting for more is safe)
-CTN_DEV void du_vmwait(int n) {
-  switch (n < 0 ? 0 : n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
-    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
   }
 }
 

@@ -35,6 +35,16 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 #define CTN_WS_GRID 256
 #endif
 constexpr int WS_WAVES = 8, WS_TM = 16, WS_GRID = CTN_WS_GRID;
+// Plain-operand configurations without a residual stream (the forward 1x1 conv, the
+// mask conv) take their tiles by LDS-DMA into a WS_DR-deep ring (CTN_WS_DMA=0: the
+// register-staged pipeline, for A/B builds)
+#ifndef CTN_WS_DMA
+#define CTN_WS_DMA 1
+#endif
+#ifndef CTN_WS_DR
+#define CTN_WS_DR 4
+#endif
+constexpr int WS_DR = CTN_WS_DR;
 constexpr int WS_FOLD_MAX = 512;   // utterances whose gLN operand stats a workgroup holds in LDS
 
 // Bound-finding experiments only (tools/microbench): bit 0 drops the output
@@ -114,7 +124,8 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
   // one tile meet in LDS and are summed after the next barrier (tile parity buffers)
   constexpr bool CLN_FIN = EPI == EPI_PRELU_STATS && NK == NORM_CLN && !SWP && S == 1;
   __shared__ double2 scln[CLN_FIN ? 2 * TM * WV : 1];
-  __shared__ __attribute__((aligned(16))) char sA[2][TM * KR * 2];
+  constexpr bool WDMA = CTN_WS_DMA && OPK == OP_PLAIN && !SWP && EPI != EPI_RESID && EPI != EPI_NORM_BWD;
+  __shared__ __attribute__((aligned(16))) char sA[WDMA ? WS_DR : 2][TM * KR * 2];
   __shared__ float sgam[EPI == EPI_NORM_BWD ? NB * 16 * WV : 1];
   // gLN operand statistics, one pair per utterance, finalized here (StatFold)
   constexpr bool FOLDS = NK == NORM_GLN && OPK != OP_PLAIN;
@@ -525,7 +536,45 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
 #endif
   // LE1 = (alpha <= 1) selects the exact two-instruction PReLU form once per kernel
   auto run = [&](auto le1) __attribute__((always_inline)) {
-    if constexpr (!SWP) {
+    if constexpr (WDMA) {
+      // The tile's image arrives by LDS-DMA WS_DR-1 tiles ahead, with no registers and
+      // no staging pass (the rows of padded frames are zero in a plain operand already).
+      // Fragment f = wid + WV*i of every tile is this wave's: lane (lg, x) of the 1-KiB
+      // fragment image holds row mb*16 + (x ^ (lg + 4(kb&3))), k-chunk 4kb + lg, the
+      // ws_slot layout.  Per tile: wait for this wave's DMA of tile t (counted: the DMA
+      // instructions of the later tiles and the output stores issued since may stay in
+      // flight; optional stores only make the wait stricter), barrier, DMA of tile
+      // t+WS_DR-1 into the slot tile t-1 was read from, MFMAs, epilogue, stores.
+      constexpr int NF = MB * KB, NFW = NF / WV, SPT = MB * Q;
+      static_assert(NF % WV == 0, "whole fragments per wave");
+      static_assert(NFW * (WS_DR - 2) + SPT * (WS_DR - 1) <= 23, "vmcnt range of vmwait23");
+      uint32_t voff[NFW];
+#pragma unroll
+      for (int i = 0; i < NFW; ++i) {
+        const int f = wid + WV * i, mb = f / KB, kb = f % KB, lq = lane >> 4;
+        const int row = mb * 16 + ((lane & 15) ^ (lq + 4 * (kb & 3)));
+        voff[i] = (uint32_t)(row * p.lda + (kb * 4 + lq) * 8) * 2u;
+      }
+      auto dma = [&](int t) __attribute__((always_inline)) {
+        if (t >= t1) return;
+        const rsrc_t rs = du_rsrc(A + (size_t)t * TM * p.lda, (long)TM * p.lda * 2);
+#pragma unroll
+        for (int i = 0; i < NFW; ++i) du_dma16(rs, sA[t % WS_DR] + (wid + WV * i) * 1024, voff[i], 0);
+      };
+      auto mn = [](int a, int b) { return a < b ? a : b; };
+      f32x4_t acc[MB][NB];
+      for (int i = 0; i < WS_DR - 1; ++i) dma(t0 + i);
+      for (int t = t0; t < t1; ++t) {
+        vmwait23(NFW * mn(WS_DR - 2, t1 - 1 - t) + SPT * mn(WS_DR - 1, t - t0));
+        lds_barrier();
+        if (t > t0) cln_final(t - 1);
+        dma(t + WS_DR - 1);
+        mfma_tile(sA[t % WS_DR], acc);
+        __builtin_amdgcn_sched_barrier(0);
+        epilogue_math(le1, t, acc);
+        store_out(t);
+      }
+    } else if constexpr (!SWP) {
       f32x4_t acc[MB][NB];
       // prologue: tiles t0 .. t0+PF-1 into slots 0 .. PF-1; t0 staged; t0+PF into slot 0
       static_for<PF>([&](auto i) { load_a(clampt(t0 + decltype(i)::value), i); });
