@@ -155,17 +155,22 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
     }
   }
 
-  float w[P][8], g1[8], b1[8];
+  // per-element arithmetic in channel pairs (f32x2: v_pk_fma/mul/add_f32), as dw_bwd
+  f32x2_t w[P][4], g1[4], b1[4];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int ch = c * 8 + e;
-    g1[e] = a.gamma1[ch];
-    b1[e] = a.beta1[ch];
+  for (int i = 0; i < 4; ++i) {
+    const int ch = c * 8 + 2 * i;
+    g1[i] = f32x2_t{a.gamma1[ch], a.gamma1[ch + 1]};
+    b1[i] = f32x2_t{a.beta1[ch], a.beta1[ch + 1]};
 #pragma unroll
-    for (int p = 0; p < P; ++p) w[p][e] = a.wd[ch * P + p];
+    for (int p = 0; p < P; ++p) w[p][i] = f32x2_t{a.wd[ch * P + p], a.wd[(ch + 1) * P + p]};
   }
+  auto pr2 = [](f32x2_t x, float al) __attribute__((always_inline)) {
+    const f32x2_t ax = x * al;
+    return f32x2_t{x[0] > 0.f ? x[0] : ax[0], x[1] > 0.f ? x[1] : ax[1]};
+  };
   // window win[i] = n1 at comb step j + (i - POWN), i in [0, P)
-  float win[P][8];
+  f32x2_t win[P][4];
   auto row_of = [&](int j) { return it.rho + j * dil; };
   // cLN: the row's statistics are fetched with the row (not at the point of use,
   // where the dependent load would stall every comb step)
@@ -176,9 +181,12 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
     r.load(h1 + (size_t)row * H + c * 8);
     st = NK == NORM_GLN ? st1u : a.st1[row];
   };
-  auto finish = [&](const Raw8<T>& r, bool ok, float2 st, float* out) {
+  auto finish = [&](const Raw8<T>& r, bool ok, float2 st, f32x2_t* out) {
+    const f32x2_t nm = {-st.x, -st.x};
+    const float okf = ok ? 1.f : 0.f;   // rows outside the utterance: 0 (their inputs are finite)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) out[e] = ok ? (prelu(r[e], al1) - st.x) * st.y * g1[e] + b1[e] : 0.f;
+    for (int i = 0; i < 4; ++i)
+      out[i] = pfma((pr2(f32x2_t{r[2 * i], r[2 * i + 1]}, al1) + nm) * st.y, g1[i], b1[i]) * okf;
   };
 #pragma unroll
   for (int i = 0; i < P - 1; ++i) {           // prologue: steps j0-POWN .. j0+P-2-POWN
@@ -221,21 +229,26 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
     if (j + D < it.j1) fetch(j + D + P - 1 - POWN, pre[q], pok[q], prow[q], pst[q]);
     finish(cur, cok, cst, win[P - 1]);
     const int k = row_of(j);
-    float out[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const f32x2_t z2 = {0.f, 0.f};
+    f32x2_t o2[4] = {z2, z2, z2, z2};
     float s = 0.f, ss = 0.f;
     if (k < K) {
 #pragma unroll
-      for (int p = 0; p < P; ++p)
+      for (int i = 0; i < 4; ++i) {
+        o2[i] = w[0][i] * win[0][i];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) out[e] += w[p][e] * win[p][e];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float a2 = prelu(out[e], al2);
-        s += a2;
-        ss += a2 * a2;
+        for (int p = 1; p < P; ++p) o2[i] = pfma(w[p][i], win[p][i], o2[i]);
+        const f32x2_t a2 = pr2(o2[i], al2);
+        s += a2[0];   // sums over the 8 channels in channel order
+        ss = fmaf(a2[0], a2[0], ss);
+        s += a2[1];
+        ss = fmaf(a2[1], a2[1], ss);
       }
     }
-    if (k < Kp) Vec8<T>::store(dout + (size_t)(it.base + k) * H + c * 8, out);
+    if (k < Kp) {
+      const float out[8] = {o2[0][0], o2[0][1], o2[1][0], o2[1][1], o2[2][0], o2[2][1], o2[3][0], o2[3][1]};
+      Vec8<T>::store(dout + (size_t)(it.base + k) * H + c * 8, out);
+    }
     if constexpr (NK == NORM_GLN) {
       ts += s;
       tss += ss;
@@ -266,7 +279,7 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
 #pragma unroll
     for (int i = 0; i < P - 1; ++i)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) win[i][e] = win[i + 1][e];
+      for (int e = 0; e < 4; ++e) win[i][e] = win[i + 1][e];
   }
   if constexpr (NK != NORM_GLN)
     if (wave_item && it.j1 > pk.j0) park_flush(it.j1 - pk.j0);
@@ -305,26 +318,35 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
     sm2u = f.slab ? fold_stat(f, it.m) : a.sm2[it.m];
   }
 
-  float w[P][8], g1[8], b1[8], g2[8];
+  // Per-element arithmetic in channel pairs (f32x2: v_pk_fma/mul/add_f32, two channels
+  // per instruction; this kernel is VALU-issue-bound at 2 waves per SIMD).  Pair i
+  // holds channels 2i, 2i+1 of the lane's 8.
+  f32x2_t w[P][4], g1[4], b1[4], g2[4];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int ch = c * 8 + e;
-    g1[e] = a.gamma1[ch];
-    b1[e] = a.beta1[ch];
-    g2[e] = a.gamma2[ch];
+  for (int i = 0; i < 4; ++i) {
+    const int ch = c * 8 + 2 * i;
+    g1[i] = f32x2_t{a.gamma1[ch], a.gamma1[ch + 1]};
+    b1[i] = f32x2_t{a.beta1[ch], a.beta1[ch + 1]};
+    g2[i] = f32x2_t{a.gamma2[ch], a.gamma2[ch + 1]};
 #pragma unroll
-    for (int p = 0; p < P; ++p) w[p][e] = a.wd[ch * P + p];
+    for (int q = 0; q < P; ++q) w[q][i] = f32x2_t{a.wd[ch * P + q], a.wd[(ch + 1) * P + q]};
   }
   // cgam/cbet: norm-1 affine gradients; cgam2/cbet2: norm-2 affine gradients
   // (sum over own rows of g_n2 * hat a2 and of g_n2)
-  float cgam[8], cbet[8], cgam2[8], cbet2[8], cwd[P][8];
+  f32x2_t cgam[4], cbet[4], cgam2[4], cbet2[4], cwd[P][4];
+  const f32x2_t z2 = {0.f, 0.f};
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    cgam[e] = cbet[e] = cgam2[e] = cbet2[e] = 0.f;
+  for (int i = 0; i < 4; ++i) {
+    cgam[i] = cbet[i] = cgam2[i] = cbet2[i] = z2;
 #pragma unroll
-    for (int p = 0; p < P; ++p) cwd[p][e] = 0.f;
+    for (int q = 0; q < P; ++q) cwd[q][i] = z2;
   }
   float calpha = 0.f, ts = 0.f, tss = 0.f;
+  // PReLU and its derivatives on a pair (exact selects, any alpha)
+  auto pr2 = [](f32x2_t x, float al) __attribute__((always_inline)) {
+    const f32x2_t ax = x * al;
+    return f32x2_t{x[0] > 0.f ? x[0] : ax[0], x[1] > 0.f ? x[1] : ax[1]};
+  };
 
   auto row_of = [&](int j) { return it.rho + j * dil; };
   // gd stream: d and dL/d(hat a2) of one comb step
@@ -337,20 +359,24 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
     rd.load(dd + (size_t)row * H + c * 8);
     rg.load(ga2 + (size_t)row * H + c * 8);
   };
-  auto finish_g = [&](const Raw8<T>& rd, const Raw8<T>& rg, bool ok, int row, bool count, float* gd) {
+  auto finish_g = [&](const Raw8<T>& rd, const Raw8<T>& rg, bool ok, int row, bool count, f32x2_t* gd) {
     const float2 st = NK == NORM_GLN ? st2u : a.st2[row];
     const float2 sm = NK == NORM_GLN ? sm2u : a.sm2[row];
+    const f32x2_t nm = {-st.x, -st.x}, nsx = {-sm.x, -sm.x}, nsy = {-sm.y, -sm.y};
+    const float okf = ok ? 1.f : 0.f;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float x = rd[e];
-      const float ah = (prelu(x, al2) - st.x) * st.y;
-      const float gn = rg[e];                                   // dL/d(norm2 output)
-      const float ga = st.y * (gn * g2[e] - sm.x - ah * sm.y);  // dL/da2
-      gd[e] = ok ? ga * prelu_dx(x, al2) : 0.f;
+    for (int i = 0; i < 4; ++i) {
+      const f32x2_t x = {rd[2 * i], rd[2 * i + 1]};
+      const f32x2_t ah = (pr2(x, al2) + nm) * st.y;                       // hat a2
+      const f32x2_t gn = {rg[2 * i], rg[2 * i + 1]};                     // dL/d(norm2 output)
+      const f32x2_t ga = pfma(ah, nsy, pfma(gn, g2[i], nsx)) * st.y;     // dL/da2
+      const f32x2_t dx = {x[0] > 0.f ? 1.f : al2, x[1] > 0.f ? 1.f : al2};
+      gd[i] = (ga * dx) * okf;   // rows outside the utterance: 0 (their inputs are finite)
       if (ok && count) {
-        calpha += ga * prelu_da(x);
-        cgam2[e] += gn * ah;
-        cbet2[e] += gn;
+        calpha = fmaf(ga[0], x[0] > 0.f ? 0.f : x[0], calpha);   // channel order
+        calpha = fmaf(ga[1], x[1] > 0.f ? 0.f : x[1], calpha);
+        cgam2[i] = pfma(gn, ah, cgam2[i]);
+        cbet2[i] += gn;
       }
     }
   };
@@ -361,13 +387,14 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
     row = it.base + (ok ? k : 0);
     rh.load(h1 + (size_t)row * H + c * 8);
   };
-  auto finish_h = [&](const Raw8<T>& rh, int row, float* ah) {
+  auto finish_h = [&](const Raw8<T>& rh, int row, f32x2_t* ah) {
     const float2 st = NK == NORM_GLN ? st1u : a.st1[row];
+    const f32x2_t nm = {-st.x, -st.x};
 #pragma unroll
-    for (int e = 0; e < 8; ++e) ah[e] = (prelu(rh[e], al1) - st.x) * st.y;
+    for (int i = 0; i < 4; ++i) ah[i] = (pr2(f32x2_t{rh[2 * i], rh[2 * i + 1]}, al1) + nm) * st.y;
   };
 
-  float gdw[P][8], ahw[P][8];
+  f32x2_t gdw[P][4], ahw[P][4];
   bool ahok[P];
 #pragma unroll
   for (int i = 0; i < P - 1; ++i) {
@@ -416,30 +443,39 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
     finish_h(ch, crowh, ahw[P - 1]);
     ahok[P - 1] = cokh;
     const int k = row_of(j);
-    float ga1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    f32x2_t ga1[4] = {z2, z2, z2, z2};
     float s = 0.f, ss = 0.f;
     if (k < K) {
-      float gn1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      f32x2_t gn1[4];
 #pragma unroll
-      for (int p = 0; p < P; ++p)
+      for (int i = 0; i < 4; ++i) {
+        gn1[i] = w[0][i] * gdw[P - 1][i];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) gn1[e] += w[p][e] * gdw[P - 1 - p][e];
+        for (int q = 1; q < P; ++q) gn1[i] = pfma(w[q][i], gdw[P - 1 - q][i], gn1[i]);
+      }
 #pragma unroll
-      for (int p = 0; p < P; ++p)
+      for (int q = 0; q < P; ++q) {
+        const float okq = ahok[q] ? 1.f : 0.f;   // window rows outside the utterance add 0
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
-          cwd[p][e] += ahok[p] ? gdw[P - 1 - POWN][e] * (ahw[p][e] * g1[e] + b1[e]) : 0.f;
+        for (int i = 0; i < 4; ++i)
+          cwd[q][i] = pfma(gdw[P - 1 - POWN][i] * okq, pfma(ahw[q][i], g1[i], b1[i]), cwd[q][i]);
+      }
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float ah = ahw[POWN][e];
-        cgam[e] += gn1[e] * ah;
-        cbet[e] += gn1[e];
-        ga1[e] = gn1[e] * g1[e];
-        s += ga1[e];
-        ss += ga1[e] * ah;
+      for (int i = 0; i < 4; ++i) {
+        const f32x2_t ah = ahw[POWN][i];
+        cgam[i] = pfma(gn1[i], ah, cgam[i]);
+        cbet[i] += gn1[i];
+        ga1[i] = gn1[i] * g1[i];
+        s += ga1[i][0];   // sums over the 8 channels in channel order
+        ss = fmaf(ga1[i][0], ah[0], ss);
+        s += ga1[i][1];
+        ss = fmaf(ga1[i][1], ah[1], ss);
       }
     }
-    if (k < Kp) Vec8<T>::store(ga1o + (size_t)(it.base + k) * H + c * 8, ga1);
+    if (k < Kp) {
+      const float o[8] = {ga1[0][0], ga1[0][1], ga1[1][0], ga1[1][1], ga1[2][0], ga1[2][1], ga1[3][0], ga1[3][1]};
+      Vec8<T>::store(ga1o + (size_t)(it.base + k) * H + c * 8, o);
+    }
     if constexpr (NK == NORM_GLN) {
       ts += s;
       tss += ss;
@@ -467,7 +503,7 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
     for (int i = 0; i < P - 1; ++i) {
       ahok[i] = ahok[i + 1];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
+      for (int e = 0; e < 4; ++e) {
         gdw[i][e] = gdw[i + 1][e];
         ahw[i][e] = ahw[i + 1][e];
       }
@@ -478,15 +514,28 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
   // ---- workgroup reductions: column partials, alpha2, norm1 sums
   const int cgn = gm.cg, nrl = 256 / cgn, rl = threadIdx.x / cgn;
   float* cs = a.col_slab + (size_t)blockIdx.x * dw_col_stride(a);
-  col_reduce8(buf, cgam, rl, c, nrl, cgn, true, cs);
-  col_reduce8(buf, cbet, rl, c, nrl, cgn, true, cs + H);
-  col_reduce8(buf, cgam2, rl, c, nrl, cgn, true, cs + (2 + P) * H);
-  col_reduce8(buf, cbet2, rl, c, nrl, cgn, true, cs + (3 + P) * H);
+  auto unpair = [](const f32x2_t (&v)[4], float (&o)[8]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { o[2 * i] = v[i][0]; o[2 * i + 1] = v[i][1]; }
+  };
+  {
+    float o[8];
+    unpair(cgam, o);
+    col_reduce8(buf, o, rl, c, nrl, cgn, true, cs);
+    unpair(cbet, o);
+    col_reduce8(buf, o, rl, c, nrl, cgn, true, cs + H);
+    unpair(cgam2, o);
+    col_reduce8(buf, o, rl, c, nrl, cgn, true, cs + (2 + P) * H);
+    unpair(cbet2, o);
+    col_reduce8(buf, o, rl, c, nrl, cgn, true, cs + (3 + P) * H);
+  }
 #pragma unroll
   for (int p = 0; p < P; ++p) {
     // stored [H][P] to match the parameter layout [H,1,P]
+    float o[8];
+    unpair(cwd[p], o);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) buf[rl * H + c * 8 + e] = cwd[p][e];
+    for (int e = 0; e < 8; ++e) buf[rl * H + c * 8 + e] = o[e];
     __syncthreads();
     for (int chn = threadIdx.x; chn < H; chn += blockDim.x) {
       float sacc = 0.f;
