@@ -10,6 +10,10 @@ under torchrun, DDP over RCCL (weak scaling: per-GPU batch fixed).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
+With --gpus N > 1 and no WORLD_SIZE in the environment (no torchrun), bench.py
+starts the N ranks itself as child processes (spawn_ranks); under torchrun it
+is one of the ranks.
+
 Prints ONE JSON line (rank 0).  `roofline` is measured live: the dominant
 kernel's launches inside the timed region are bracketed by hipEvents on their
 own stream (ctn_timer_*), and achieved = algorithmic bytes per launch / mean
@@ -81,27 +85,32 @@ def step_flops(M, K, cfg):
 
 
 def _cpu_model():
-    """CPU model name and the physical cores this process may run on (lscpu's view)."""
-    name, cores = "unknown", set()
+    """CPU model name, the host's physical cores, the logical CPUs this process may run
+    on, and the physical cores among those (lscpu's view, from /proc/cpuinfo)."""
+    name, cores, core_of = "unknown", set(), {}
     try:
         with open("/proc/cpuinfo") as f:
-            phys = core = None
-            for line in f:
+            proc = phys = core = None
+            for line in f.read().splitlines() + [""]:
                 k, _, v = line.partition(":")
                 k, v = k.strip(), v.strip()
-                if k == "model name" and name == "unknown":
+                if k == "processor":
+                    proc = int(v)
+                elif k == "model name" and name == "unknown":
                     name = v
                 elif k == "physical id":
                     phys = v
                 elif k == "core id":
                     core = v
-                elif not k and phys is not None:
+                elif not k and proc is not None:
                     cores.add((phys, core))
-                    phys = core = None
+                    core_of[proc] = (phys, core)
+                    proc = phys = core = None
     except OSError:
         pass
-    allowed = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    return name, len(cores) or None, allowed
+    allowed = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
+    phys_allowed = len({core_of.get(c, c) for c in allowed})
+    return name, len(cores) or None, len(allowed), phys_allowed
 
 
 def _time_train_steps(cfg_d, T, seconds):
@@ -121,20 +130,69 @@ def _time_train_steps(cfg_d, T, seconds):
             return n, el
 
 
-def cpu_baseline(seconds=12.0):
+def cpu_baseline(seconds=10.0):
     """fp32 CPU oracle train step (fwd + loss + bwd + clip + Adam), M=1, on this box's host
-    cores: the paper config (the reported value) and c1 (BASELINE.json configs[0])."""
-    threads = torch.get_num_threads()
-    name, phys, allowed = _cpu_model()
-    n, el = _time_train_steps(PAPER, 32000, seconds)
-    n1, el1 = _time_train_steps(dict(PAPER, N=64, B=64, H=128, X=2, R=2), 32000, seconds / 3)
-    return {"value": n / el, "unit": "utterances/sec", "cores": threads, "kind": "port",
+    cores: the paper config (the reported value) and c1 (BASELINE.json configs[0]).
+
+    SURVEY.md §8(d): torch.set_num_threads(n), n = the physical cores this process may
+    run on.  The step is also timed at the process's default thread count (the box's
+    per-GPU CPU share, OMP_NUM_THREADS); `value` is the faster of the two, and both are
+    recorded."""
+    default_threads = torch.get_num_threads()
+    name, phys, allowed, phys_allowed = _cpu_model()
+    runs = {}
+    try:
+        for threads in sorted({phys_allowed, default_threads}, reverse=True):
+            torch.set_num_threads(threads)
+            n, el = _time_train_steps(PAPER, 32000, seconds)
+            runs[threads] = (n, el)
+        best = max(runs, key=lambda th: runs[th][0] / runs[th][1])
+        torch.set_num_threads(best)
+        n1, el1 = _time_train_steps(dict(PAPER, N=64, B=64, H=128, X=2, R=2), 32000, seconds / 3)
+    finally:
+        torch.set_num_threads(default_threads)
+    n, el = runs[best]
+    return {"value": n / el, "unit": "utterances/sec", "cores": best, "kind": "port",
             "cpu": name, "physical_cores_on_host": phys, "cpus_allowed": allowed,
+            "physical_cores_allowed": phys_allowed,
+            "by_threads": {str(th): round(v[0] / v[1], 3) for th, v in runs.items()},
             "sample": f"{n} training steps (fwd+PIT loss+bwd+clip+Adam) of 1 utterance, paper config, "
-                      f"4 s @ 8 kHz, fp32 oracle/ctn_oracle.py on {threads} threads, {el:.1f} s",
+                      f"4 s @ 8 kHz, fp32 oracle/ctn_oracle.py on {best} threads, {el:.1f} s "
+                      f"(faster of {sorted(runs)} threads; {phys_allowed} physical cores allowed)",
             "c1": {"value": n1 / el1, "unit": "utterances/sec",
                    "sample": f"{n1} c1 training steps (N=64 B=64 H=128 X=2 R=2), 1 utterance 4 s @ 8 kHz, "
-                             f"{el1:.1f} s"}}
+                             f"{best} threads, {el1:.1f} s"}}
+
+
+def spawn_ranks(n, cmd, port=None, env=None):
+    """Start `cmd` as n ranks of one job (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*), wait for
+    all of them and return the first non-zero exit code (0 when every rank succeeded).
+
+    The parent never touches the GPU and never execs: each rank is a fresh child process
+    (the reference's multi-GPU path, src/train.py:120-122, is nn.DataParallel over the
+    --id GPUs inside one process; here one process per GPU, DDP over RCCL)."""
+    import socket
+    import subprocess
+    if port is None:
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+    base = dict(os.environ if env is None else env)
+    base.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n),
+                LOCAL_WORLD_SIZE=str(n))
+    procs = []
+    for r in range(n):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen(cmd, env=e))
+    rc = 0
+    for p in procs:
+        code = p.wait()
+        if code and not rc:
+            rc = code
+            for q in procs:              # one rank failed: the others would wait forever
+                if q.poll() is None:
+                    q.terminate()
+    return rc
 
 
 def main():
@@ -153,13 +211,23 @@ def main():
                     help="DDP over RCCL even at world size 1 (exercises process-group init, bucket hooks)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no outside launcher: start one rank per GPU ourselves (children, no exec);
+        # counting devices does not initialise the GPU in this (parent) process
+        visible = torch.cuda.device_count()
+        if args.gpus > visible:
+            sys.exit(f"bench.py: --gpus {args.gpus} but only {visible} GPU(s) visible")
+        sys.exit(spawn_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world and "WORLD_SIZE" in os.environ and args.gpus != 1:
+        sys.exit(f"bench.py: --gpus {args.gpus} disagrees with WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_ddp = world > 1 or args.ddp
     if use_ddp:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        world = dist.get_world_size()    # what RCCL reports
     dev = torch.device("cuda", local)
 
     import conv_tasnet as ct
@@ -268,11 +336,11 @@ def main():
                        "parallelism": f"dp{world}" + (" (DDP/RCCL)" if use_ddp else "")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": {1: "gemm_rows fwd 1x1 B->H (PReLU-stats epilogue)",
+                         "kernel": {1: "gemm_ws fwd 1x1 B->H (PReLU-stats epilogue)",
                                     2: "dw_fwd (norm1+depthwise+stats)",
                                     3: ("gemm_dual bwd g_n2 = gy.W2 (norm-backward epilogue) + dW2 = gy^T.n2"
                                         if dual_pair_a() else
-                                        "gemm_rows bwd g_n2 = gy.W2 (norm-backward epilogue)")}[args.timer_kind],
+                                        "gemm_ws bwd g_n2 = gy.W2 (norm-backward epilogue)")}[args.timer_kind],
                          "launches": nl.value, "mean_ms": round(mean_ms, 4), "bytes_per_launch": kb,
                          # rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * 1024 SIMDs) of
                          # this kernel, from the committed PMC pass (profiles/pmc_mfma.json)
