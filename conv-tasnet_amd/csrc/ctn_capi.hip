@@ -794,7 +794,7 @@ static int codec_check(const ctn_codec_desc* d, bool need_b) {
   if (d->N % 8 || cg > 64 || (cg & (cg - 1)))
     return fail(CTN_ERR_UNSUPPORTED, "N=%d: need N/8 a power of two <= 64", d->N);
   if (need_b && (d->B % 8 || d->B < 8)) return fail(CTN_ERR_UNSUPPORTED, "B=%d must be a multiple of 8", d->B);
-  if (d->C < 1 || d->C > 4) return fail(CTN_ERR_UNSUPPORTED, "C=%d outside 1..4", d->C);
+  if (d->C < 1 || d->C > 8) return fail(CTN_ERR_UNSUPPORTED, "C=%d outside 1..8", d->C);
   if (d->mask_type < 0 || d->mask_type > 2) return fail(CTN_ERR_ARG, "mask_type %d", d->mask_type);
   if (d->dtype != CTN_DTYPE_F32 && d->dtype != CTN_DTYPE_BF16) return fail(CTN_ERR_ARG, "dtype %d", d->dtype);
   return CTN_OK;
@@ -850,7 +850,7 @@ EncLayout enc_layout(const ctn_codec_desc* d, int backward, void* ws) {
       L.tmpU = c.take<float>((size_t)d->N * L.Lp * sizeof(float));
     } else {
       L.gpre = c.take<float>((size_t)rows * d->N * sizeof(float));
-      L.nU = frame_outer_chunks(a);
+      L.nU = frame_outer_chunks(a, 1);
       L.slabU = c.take<float>((size_t)L.nU * d->N * d->L * sizeof(float));
     }
     GemmCols gc{};
@@ -1006,7 +1006,7 @@ DecLayout dec_layout(const ctn_codec_desc* d, int backward, bool with_mask_conv,
       L.chunksV = gemm_cols_default_chunks(dv_gemm(d, L.Lp));
       L.cpartV = c.take<float>((size_t)L.chunksV * L.Lp * d->N * sizeof(float));
     } else {
-      L.nV = frame_outer_chunks(a);
+      L.nV = frame_outer_chunks(a, d->C);
       L.slabV = c.take<float>((size_t)L.nV * d->N * d->L * sizeof(float));
     }
     if (with_mask_conv) {
@@ -1127,9 +1127,12 @@ static int pit_chunks(int T) {
   return c < 1 ? 1 : (c > 64 ? 64 : c);
 }
 
+constexpr int PIT_CMAX = 8;   // C! = 40,320 permutations
+
 static void pit_perms(PitArgs& a) {
   int p[4] = {0, 1, 2, 3};
   a.nperm = 0;
+  if (a.C > 4) return;          // pit_final_wide decodes them on the device
   // lexicographic order == itertools.permutations(range(C)) (pit_criterion.py:66)
   do {
     for (int i = 0; i < a.C; ++i) a.perms[a.nperm][i] = p[i];
@@ -1145,15 +1148,15 @@ static void pit_perms(PitArgs& a) {
 }
 
 extern "C" size_t ctn_pit_workspace_bytes(const ctn_pit_desc* d) {
-  if (!d || d->M < 1 || d->C < 1 || d->C > 4 || d->T < 1) return 0;
-  return (size_t)d->M * pit_chunks(d->T) * pit_nv(d->C) * sizeof(double) + 256;
+  if (!d || d->M < 1 || d->C < 1 || d->C > PIT_CMAX || d->T < 1) return 0;
+  return (size_t)d->M * pit_chunks(d->T) * pit_nv(d->C) * sizeof(double) + (size_t)d->M * sizeof(double) + 256;
 }
 
 extern "C" int ctn_pit_forward(const ctn_pit_desc* d, const float* source, float* est, const int64_t* lengths,
                                float* loss, float* max_snr, int64_t* best_perm, float* reordered, float* coef,
                                void* ws, size_t ws_bytes, void* stream) {
   if (!d || d->M < 1 || d->C < 1 || d->T < 1) return fail(CTN_ERR_ARG, "bad PIT descriptor");
-  if (d->C > 4) return fail(CTN_ERR_UNSUPPORTED, "C=%d > 4 speakers", d->C);
+  if (d->C > PIT_CMAX) return fail(CTN_ERR_UNSUPPORTED, "C=%d > %d speakers", d->C, PIT_CMAX);
   if (!source || !est || !lengths || !loss || !max_snr || !best_perm || !coef) return fail(CTN_ERR_ARG, "null pointer");
   if (!ws || ws_bytes < ctn_pit_workspace_bytes(d)) return fail(CTN_ERR_WORKSPACE, "PIT workspace too small");
   PitArgs a{};
@@ -1161,6 +1164,7 @@ extern "C" int ctn_pit_forward(const ctn_pit_desc* d, const float* source, float
   a.src = source; a.est = est; a.lengths = lengths;
   a.slab = reinterpret_cast<double*>(ws);
   a.chunks = pit_chunks(d->T);
+  a.msd = a.slab + (size_t)d->M * a.chunks * pit_nv(d->C);
   a.max_snr = max_snr; a.best = best_perm; a.coef = coef; a.loss = loss;
   a.est_inplace = est; a.reordered = reordered;
   pit_perms(a);
@@ -1171,7 +1175,8 @@ extern "C" int ctn_pit_forward(const ctn_pit_desc* d, const float* source, float
 extern "C" int ctn_pit_backward(const ctn_pit_desc* d, const float* source, const float* est,
                                 const int64_t* lengths, const float* coef, const float* g_loss,
                                 const float* g_max_snr, float* g_est, void* stream) {
-  if (!d || d->M < 1 || d->C < 1 || d->C > 4 || d->T < 1) return fail(CTN_ERR_ARG, "bad PIT descriptor");
+  if (!d || d->M < 1 || d->C < 1 || d->T < 1) return fail(CTN_ERR_ARG, "bad PIT descriptor");
+  if (d->C > PIT_CMAX) return fail(CTN_ERR_UNSUPPORTED, "C=%d > %d speakers", d->C, PIT_CMAX);
   if (!source || !est || !lengths || !coef || !g_est) return fail(CTN_ERR_ARG, "null pointer");
   PitArgs a{};
   a.M = d->M; a.C = d->C; a.T = d->T;

@@ -43,7 +43,7 @@ hipError_t launch_unpad_cols(const float* tmp, int N, int Lp, int L, float* out,
 
 hipError_t launch_enc_fwd(DType dt, const CodecArgs& a, hipStream_t s);
 hipError_t launch_enc_bwd_rows(DType dt, const CodecArgs& a, hipStream_t s);
-int frame_outer_chunks(const CodecArgs& a);
+int frame_outer_chunks(const CodecArgs& a, int C);   // C: rows of sources per frame (encoder 1)
 hipError_t launch_frame_outer(DType dt, int mode, const CodecArgs& a, hipStream_t s);
 hipError_t launch_dec_fwd(DType dt, const CodecArgs& a, hipStream_t s);
 hipError_t launch_dec_bwd(DType dt, const CodecArgs& a, hipStream_t s);
@@ -65,8 +65,9 @@ struct PitArgs {
   float* gest;                   // [M][C][T] (backward)
   float* est_inplace;            // est to mask in place (forward)
   float* reordered;              // [M][C][T]
+  double* msd;                   // [M] max_snr in fp64 (C > 4: pit_final_wide -> pit_loss)
   int nperm;
-  int perms[24][4];              // lexicographic permutations of range(C)
+  int perms[24][4];              // lexicographic permutations of range(C) (C <= 4)
 };
 int pit_nv(int C);
 hipError_t launch_pit_forward(const PitArgs& a, hipStream_t s);

@@ -174,8 +174,11 @@ __global__ __launch_bounds__(256) void enc_bwd_rows_kernel(CodecArgs a) {
 // ===========================================================================
 constexpr int FO_R = 16, FO_WGS = 512, FO_LMAX = 32;
 
-template <typename T, int MODE, int LT>   // LT: compile-time L (0: generic, <= FO_LMAX)
+// LT: compile-time L (0: generic, <= FO_LMAX); CM: speakers held per row (4, or 8 for
+// 5 <= C <= 8, with FO_R / 2 rows per chunk so the staged rows stay within LDS)
+template <typename T, int MODE, int LT, int CM = 4>
 __global__ __launch_bounds__(256) void frame_outer_kernel(CodecArgs a) {
+  constexpr int FO_R = CM > 4 ? ctn::FO_R / 2 : ctn::FO_R;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   constexpr int LL = LT ? LT : FO_LMAX;
   const int N = a.N, L = LT ? LT : a.L, S = a.S, C = MODE == 0 ? 1 : a.C, K = a.K, Kp = a.Kp;
@@ -201,7 +204,7 @@ __global__ __launch_bounds__(256) void frame_outer_kernel(CodecArgs a) {
     for (int i = threadIdx.x; i < FO_R * cg; i += 256) {
       const int rr = i / cg, c8 = i % cg, k = kb + rr;
       const size_t r = (size_t)m * Kp + k;
-      float v[4][8];
+      float v[CM][8];
       if (k < K) {
         if constexpr (MODE == 0) {
           const float4 g0 = *reinterpret_cast<const float4*>(a.gpre + r * N + c8 * 8);
@@ -278,7 +281,7 @@ __global__ __launch_bounds__(256) void frame_outer_kernel(CodecArgs a) {
 // decoder forward: frames[m][c][k][l]  (fp32)
 // workgroup = DEC_RPB frame rows; src = w * act(score) staged in LDS [rows][C][N]
 // ===========================================================================
-template <typename T>
+template <typename T, int CM = 4>   // CM: speakers held per row (4 or 8)
 __global__ __launch_bounds__(256) void dec_fwd_kernel(CodecArgs a, int rpb) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int N = a.N, L = a.L, C = a.C, K = a.K, Kp = a.Kp;
@@ -295,7 +298,7 @@ __global__ __launch_bounds__(256) void dec_fwd_kernel(CodecArgs a, int rpb) {
   for (int i = threadIdx.x; i < rpb * cg; i += 256) {
     const int rr = i / cg, c8 = i % cg;
     const size_t r = (size_t)row0 + rr;
-    float wv[8], s[4][8];
+    float wv[8], s[CM][8];
     Vec8<T>::load(w + r * N + c8 * 8, wv);
     for (int cc = 0; cc < C; ++cc) Vec8<T>::load(sc + r * (size_t)(C * N) + (size_t)cc * N + c8 * 8, s[cc]);
 #pragma unroll
@@ -346,7 +349,7 @@ __global__ __launch_bounds__(256) void ola_fwd_kernel(CodecArgs a) {
 // ===========================================================================
 // decoder backward (rows): gsrc = gframes . V ; gw = sum_c gsrc_c act_c ; gscore
 // ===========================================================================
-template <typename T>
+template <typename T, int CM = 4>   // CM: speakers held per row (4 or 8)
 __global__ __launch_bounds__(256) void dec_bwd_kernel(CodecArgs a, int rpb) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int N = a.N, L = a.L, C = a.C, S = a.S, K = a.K, Kp = a.Kp;
@@ -376,7 +379,7 @@ __global__ __launch_bounds__(256) void dec_bwd_kernel(CodecArgs a, int rpb) {
       Vec8<T>::store(gw + r * N + c8 * 8, gwv);
       continue;
     }
-    float wv[8], s[4][8], ga[4][8];
+    float wv[8], s[CM][8], ga[CM][8];
     Vec8<T>::load(w + r * N + c8 * 8, wv);
     for (int cc = 0; cc < C; ++cc) Vec8<T>::load(sc + r * (size_t)(C * N) + (size_t)cc * N + c8 * 8, s[cc]);
     // gsrc[cc][e] = sum_l gf[rr][cc][l] * V[l][n]
@@ -395,7 +398,7 @@ __global__ __launch_bounds__(256) void dec_bwd_kernel(CodecArgs a, int rpb) {
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      float act[4];
+      float act[CM];
       if (a.mask_type == 1) {
         float mx = -3.4e38f, den = 0.f;
         for (int cc = 0; cc < C; ++cc) mx = fmaxf(mx, s[cc][e]);
@@ -781,7 +784,7 @@ static unsigned dm_grid(const CodecArgs& a) {
 // ===========================================================================
 static bool codec_ok(const CodecArgs& a) {
   return a.N % 8 == 0 && a.N / 8 <= 64 && ((a.N / 8) & (a.N / 8 - 1)) == 0 && a.L >= 1 && a.L <= 32 &&
-         a.S >= 1 && a.C >= 1 && a.C <= 4 && a.Kp % EN_RPB == 0;
+         a.S >= 1 && a.C >= 1 && a.C <= 8 && a.Kp % EN_RPB == 0;
 }
 
 hipError_t launch_enc_fwd(DType dt, const CodecArgs& a, hipStream_t s) {
@@ -805,19 +808,22 @@ hipError_t launch_enc_bwd_rows(DType dt, const CodecArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-int frame_outer_chunks(const CodecArgs& a) {
-  const int n = a.M * (a.Kp / FO_R);
+int frame_outer_chunks(const CodecArgs& a, int C) {
+  const int n = a.M * (a.Kp / (C > 4 ? FO_R / 2 : FO_R));
   return n < FO_WGS ? n : FO_WGS;
 }
 
 hipError_t launch_frame_outer(DType dt, int mode, const CodecArgs& a, hipStream_t s) {
-  if (!codec_ok(a) || a.Kp % FO_R || a.N > 512 || a.L > FO_LMAX || a.C > 4) return hipErrorInvalidValue;
+  if (!codec_ok(a) || a.Kp % FO_R || a.N > 512 || a.L > FO_LMAX) return hipErrorInvalidValue;
   const int C = mode == 0 ? 1 : a.C;
-  const size_t lds = ((size_t)FO_R * C * a.N + (size_t)C * (FO_R * a.S + a.L)) * sizeof(float);
-  const dim3 g(frame_outer_chunks(a)), b(256);
-#define CTN_FO(T_, M_)                                                                             \
-  if (a.L == 20) hipLaunchKernelGGL((frame_outer_kernel<T_, M_, 20>), g, b, lds, s, a);            \
-  else if (a.L == 16) hipLaunchKernelGGL((frame_outer_kernel<T_, M_, 16>), g, b, lds, s, a);       \
+  const int fr = C > 4 ? FO_R / 2 : FO_R;
+  const size_t lds = ((size_t)fr * C * a.N + (size_t)C * (fr * a.S + a.L)) * sizeof(float);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  const dim3 g(frame_outer_chunks(a, C)), b(256);
+#define CTN_FO(T_, M_)                                                                                          \
+  if (C > 4) hipLaunchKernelGGL((frame_outer_kernel<T_, M_, 0, 8>), g, b, lds, s, a);                        \
+  else if (a.L == 20) hipLaunchKernelGGL((frame_outer_kernel<T_, M_, 20>), g, b, lds, s, a);                  \
+  else if (a.L == 16) hipLaunchKernelGGL((frame_outer_kernel<T_, M_, 16>), g, b, lds, s, a);                  \
   else hipLaunchKernelGGL((frame_outer_kernel<T_, M_, 0>), g, b, lds, s, a);
   if (mode == 0) {
     if (dt == BF16) { CTN_FO(bf16raw, 0) } else { CTN_FO(float, 0) }
@@ -851,6 +857,9 @@ hipError_t launch_dec_fwd(DType dt, const CodecArgs& a, hipStream_t s) {
     }
     if (a.N == 256) { CTN_DFM(8) } else { CTN_DFM(16) }
 #undef CTN_DFM
+  } else if (a.C > 4) {
+    if (dt == BF16) hipLaunchKernelGGL((dec_fwd_kernel<bf16raw, 8>), g, b, lds, s, a, rpb);
+    else hipLaunchKernelGGL((dec_fwd_kernel<float, 8>), g, b, lds, s, a, rpb);
   } else if (dt == BF16) hipLaunchKernelGGL(dec_fwd_kernel<bf16raw>, g, b, lds, s, a, rpb);
   else hipLaunchKernelGGL(dec_fwd_kernel<float>, g, b, lds, s, a, rpb);
   hipError_t e = hipGetLastError();
@@ -898,6 +907,9 @@ hipError_t launch_dec_bwd(DType dt, const CodecArgs& a, hipStream_t s) {
     }
     if (a.N == 256) { CTN_DBM(16) } else { CTN_DBM(32) }
 #undef CTN_DBM
+  } else if (a.C > 4) {
+    if (dt == BF16) hipLaunchKernelGGL((dec_bwd_kernel<bf16raw, 8>), g, b, lds, s, a, rpb);
+    else hipLaunchKernelGGL((dec_bwd_kernel<float, 8>), g, b, lds, s, a, rpb);
   } else if (dt == BF16) hipLaunchKernelGGL(dec_bwd_kernel<bf16raw>, g, b, lds, s, a, rpb);
   else hipLaunchKernelGGL(dec_bwd_kernel<float>, g, b, lds, s, a, rpb);
   return hipGetLastError();

@@ -100,16 +100,23 @@ CTN_DEV rsrc_t du_rsrc(const void* p, long bytes) {
 CTN_DEV uint32_t du_ldsaddr(const char* p) {
   return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)p);
 }
+// CTN_DMA_TAIL: wait states after the LDS-DMA issue (diagnostic builds)
+#ifndef CTN_DMA_TAIL
+#define CTN_DMA_TAIL ""
+#endif
+#ifndef CTN_DMA_HEAD
+#define CTN_DMA_HEAD "s_nop 0\n\t"
+#endif
 CTN_DEV void du_dma16(rsrc_t r, const char* lds, uint32_t voff, int soff) {
   uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\t" CTN_DMA_HEAD "buffer_load_dwordx4 %1, %2, %4 offen lds\n\t" CTN_DMA_TAIL "s_mov_b32 m0, %0"
                : "=&s"(keep)
                : "v"(voff), "s"(r), "s"(du_ldsaddr(lds)), "s"(soff)
                : "memory");
 }
 CTN_DEV void du_dma4(rsrc_t r, const char* lds, uint32_t voff, int soff) {
   uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\t" CTN_DMA_HEAD "buffer_load_dword %1, %2, %4 offen lds\n\t" CTN_DMA_TAIL "s_mov_b32 m0, %0"
                : "=&s"(keep)
                : "v"(voff), "s"(r), "s"(du_ldsaddr(lds)), "s"(soff)
                : "memory");
@@ -259,6 +266,17 @@ CTN_DEV float wave_sum_dpp(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
 }
 
+// Sum over the four 16-lane rows of a wave (the lanes l, l^16, l^32, l^48) with
+// v_permlane16_swap / v_permlane32_swap: VALU lane exchanges, no LDS instruction
+// (a kernel with LDS-DMA in flight keeps its cross-lane traffic off the LDS unit).
+// Every lane ends with the same bits: a swap pair adds the same two values.
+CTN_DEV float xsum_rows(float v) {
+  auto q = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(q[0]) + __uint_as_float(q[1]);   // v_l + v_{l^16}
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // fp64 wave64 sum with the same DPP row operations on both halves (no ds_bpermute:
 // kernels with LDS-DMA in flight reduce this way; total read from lane 63)
 template <int CTRL, int ROW_MASK> CTN_DEV double dpp_d(double x) {
@@ -284,9 +302,9 @@ CTN_DEV double wave_sum_dpp_d(double v) {
 // IEEE maximum/minimum (NaN-propagating): one v_maximum3/v_minimum3_f32 per element on
 // gfx950, where maxnum/minnum in IEEE mode also quiet each non-arithmetic input first
 // (two more v_max_f32 per element)
-// 0 (default): maxnum/minnum as before.  1 measured neutral (fwd1 51.5 -> 51.2 us) and,
-// in the dual GEMM, moved code placement into the latent statistics race noted in
-// DESIGN.md §10
+// 0 (default): maxnum/minnum as before.  1 measured neutral (fwd1 51.5 -> 51.2 us); in
+// round 2 it moved the dual GEMM's code placement into the epilogue/LDS-DMA
+// reproducibility problem of DESIGN.md §10 (round 3: reproducible, profiles/r03/race)
 #ifndef CTN_IEEE_MAX
 #define CTN_IEEE_MAX 0
 #endif

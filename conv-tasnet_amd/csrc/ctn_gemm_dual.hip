@@ -45,14 +45,37 @@ constexpr int DU_MMAX = 512;   // utterances whose gLN statistics a workgroup ho
 #ifndef CTN_DU_EXP
 #define CTN_DU_EXP 0
 #endif
-// cLN per-row statistics: 1 = a 4-byte LDS-DMA per wave and tile into a per-wave ring
-// (measured racy on gfx950: run-to-run different norm-2 sums), 0 = plain loads from
-// L2 at the point of use (the default; deterministic).
 #ifndef CTN_DU_DA
 #define CTN_DU_DA 4   // LDS ring depth of the (256 -> 512, norm-backward) pair
 #endif
+// cLN per-row statistics: 1 = a 4-byte LDS-DMA per wave and tile into a per-wave ring,
+// with no LDS-DMA in flight while the epilogue runs (vmcnt(0) before it); 0 = plain
+// loads from L2 at the point of use (their compiler-counted waits drain the ring
+// before every use).  Both reproducible run to run; 1 is faster.
 #ifndef CTN_DU_CST_DMA
-#define CTN_DU_CST_DMA 0
+#define CTN_DU_CST_DMA 1
+#endif
+// cLN per-row sums across the four lane rows: 1 = v_permlane16/32_swap (VALU),
+// 0 = ds_bpermute (wrong sums in every launch while LDS-DMA is in flight, §10)
+#ifndef CTN_DU_PERMLANE
+#define CTN_DU_PERMLANE 1
+#endif
+// Reproducibility experiments (tools/microbench/dual_det.hip), all off:
+//   CTN_DU_DBG bit 0 vmcnt(0) before each epilogue, bit 1 vmcnt(0) at the loop top,
+//     bit 2 lgkmcnt(0) after each cross-lane step of the cLN row sums, bit 3
+//     lgkmcnt(0) after the epilogue's statistics and raw-row LDS reads, bit 4
+//     vmcnt(0) right after the cLN statistics store;
+//   CTN_DU_LATE 1: each iteration issues its DMA group after the epilogue;
+//   CTN_DU_NOCLAMP 1: the last D-1 iterations issue no DMA (default: they re-issue
+//     the range's last tile into its own slot, same bytes).
+#ifndef CTN_DU_DBG
+#define CTN_DU_DBG 0
+#endif
+#ifndef CTN_DU_LATE
+#define CTN_DU_LATE 0
+#endif
+#ifndef CTN_DU_NOCLAMP
+#define CTN_DU_NOCLAMP 0
 #endif
 
 // LDS images (byte offsets), all checked conflict-free (bank model of
@@ -139,7 +162,8 @@ __global__ __launch_bounds__(DU_NT) void gemm_dual_kernel(GemmDual p) {
   constexpr int GA = A_SZ / 1024 / WV;                 // A blocks per wave per tile
   constexpr int G = GA + 1 + (CST ? 1 : 0);            // DMA instructions per wave per tile
   constexpr int SST = EPI == EPI_NORM_BWD ? 1 : 0;     // statistics stores per wave per tile
-  constexpr int OFF_B = D * A_SZ;                      // Bm ring (raw rows or B image)
+  constexpr int OFF_A = 0;                             // A ring
+  constexpr int OFF_B = OFF_A + D * A_SZ;              // Bm ring (raw rows or B image)
   constexpr int OFF_R = OFF_B + D * B_SZ;              // residual ring (plain case)
   constexpr int OFF_BI = OFF_R + (BXF ? 0 : D * B_SZ); // B image, 2 parities (transform case)
   constexpr int OFF_C = OFF_BI + (BXF ? 2 * B_SZ : 0); // C image, 2 parities
@@ -255,7 +279,7 @@ __global__ __launch_bounds__(DU_NT) void gemm_dual_kernel(GemmDual p) {
     for (int u = 0; u < GA; ++u) {
       // rows of padded frames arrive as zeros (out-of-range offset)
       const uint32_t vo = tk + arow[u] < Kv ? avo[u] : DU_OOB;
-      du_dma16(rA, smem + slot * A_SZ + (wid * GA + u) * 1024, vo, t * TM * p.lda * 2);
+      du_dma16(rA, smem + OFF_A + slot * A_SZ + (wid * GA + u) * 1024, vo, t * TM * p.lda * 2);
     }
     if constexpr (BXF) {
       du_dma16(rB, smem + OFF_B + slot * B_SZ + wid * 1024, bvo, t * TM * p.ldb * 2);
@@ -267,18 +291,20 @@ __global__ __launch_bounds__(DU_NT) void gemm_dual_kernel(GemmDual p) {
   };
   // vmcnt that retires DMA group tq at the top of iteration t (k = t - t0): the
   // operations issued after it, by the fixed per-iteration order
-  // [C store (k >= 1), DMA group (G), statistics store (SST)]
+  // [C store (k >= 1), DMA group (G, only for tiles < t1), statistics store (SST)]
   auto ops_after = [&](int tq, int t) __attribute__((always_inline)) {
-    const int j = tq - t0, k = t - t0;
+    const int nt = t1 - t0;
+    const int j = (CTN_DU_NOCLAMP && tq > t1 - 1 ? t1 - 1 : tq) - t0, k = t - t0;
+    auto grp = [&](int jj) { return CTN_DU_NOCLAMP && jj >= nt ? 0 : G; };
     int n = 0, kfrom;
     if (j <= D - 2) {
-      n = (D - 2 - j) * G;
+      for (int jj = j + 1; jj <= D - 2; ++jj) n += grp(jj);
       kfrom = 0;
     } else {
-      n = SST;
+      n = CTN_DU_LATE ? 0 : SST;   // ops of group j's own iteration issued after it
       kfrom = j - D + 2;
     }
-    for (int kk = kfrom; kk < k; ++kk) n += (kk >= 1 ? 1 : 0) + G + SST;
+    for (int kk = kfrom; kk < k; ++kk) n += (kk >= 1 ? 1 : 0) + grp(kk + D - 1) + SST;
     return n;
   };
 
@@ -350,7 +376,7 @@ __global__ __launch_bounds__(DU_NT) void gemm_dual_kernel(GemmDual p) {
   };
 
   auto compute = [&](int t, f32x4_t (&acc)[NBW]) __attribute__((always_inline)) {
-    const char* a = smem + (t % D) * A_SZ;
+    const char* a = smem + OFF_A + (t % D) * A_SZ;
     const char* bsl = BXF ? smem + OFF_BI + (t & 1) * B_SZ : smem + OFF_B + (t % D) * B_SZ;
 #pragma unroll
     for (int nb = 0; nb < NBW; ++nb) acc[nb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -400,6 +426,7 @@ __global__ __launch_bounds__(DU_NT) void gemm_dual_kernel(GemmDual p) {
     uint32_t rw[NV / 2];
     if constexpr (NV == 8) {
       const v4u r4 = *reinterpret_cast<const v4u*>(smem + (BXF ? OFF_B : OFF_R) + slot * B_SZ + rdo);
+      if constexpr (CTN_DU_DBG & 8) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       rw[0] = r4[0]; rw[1] = r4[1]; rw[2] = r4[2]; rw[3] = r4[3];
     } else {
       const uint2 r2 = *reinterpret_cast<const uint2*>(smem + (BXF ? OFF_B : OFF_R) + slot * B_SZ + rdo);
@@ -411,6 +438,7 @@ __global__ __launch_bounds__(DU_NT) void gemm_dual_kernel(GemmDual p) {
       for (int c = 0; c < NV / 2; ++c) v2[c] += f32x2_t{__uint_as_float(rw[c] << 16), __uint_as_float(rw[c] & 0xffff0000u)};
     } else {
       const float2 est = row_stat(t, slot, erow);
+      if constexpr (CTN_DU_DBG & 8) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       const f32x2_t rs = {est.y, est.y}, ms = {-est.x * est.y, -est.x * est.y};
 #pragma unroll
       for (int c = 0; c < NV / 2; ++c) {
@@ -439,9 +467,17 @@ __global__ __launch_bounds__(DU_NT) void gemm_dual_kernel(GemmDual p) {
         run_slab[m - m0] = make_double2(run_s, run_q);
       } else {
         float s = s2[0] + s2[1], ss = q2[0] + q2[1];
+#if CTN_DU_PERMLANE
+        s = xsum_rows(s);
+        ss = xsum_rows(ss);
+#else
         s += __shfl_xor(s, 16, 64); ss += __shfl_xor(ss, 16, 64);
+        if constexpr (CTN_DU_DBG & 4) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         s += __shfl_xor(s, 32, 64); ss += __shfl_xor(ss, 32, 64);
+        if constexpr (CTN_DU_DBG & 4) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
         p.grp_slab[(size_t)(t * TM + erow) * (S * WNB) + sl * WNB + nbg] = make_double2((double)s, (double)ss);
+        if constexpr (CTN_DU_DBG & 16) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
     }
   };
@@ -465,22 +501,35 @@ __global__ __launch_bounds__(DU_NT) void gemm_dual_kernel(GemmDual p) {
   auto clampt = [&](int t) __attribute__((always_inline)) { return t < t1 ? t : t1 - 1; };
   auto run = [&](auto le1) __attribute__((always_inline)) {
     f32x4_t acc[NBW];
-    for (int i = 0; i < D - 1; ++i) dma(clampt(t0 + i));
+    for (int i = 0; i < D - 1; ++i)
+      if (!CTN_DU_NOCLAMP) dma(clampt(t0 + i));
+      else if (t0 + i < t1) dma(t0 + i);
     for (int t = t0; t < t1; ++t) {
       // BXF: the transform reads raw Bm of tile t+1 this iteration, so wait for its group
       const int tq = BXF ? t + 1 : t;
-      if constexpr (!(CTN_DU_EXP & 128)) du_vmwait(ops_after(tq, t));
+      if constexpr (CTN_DU_DBG & 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else if constexpr (!(CTN_DU_EXP & 128)) du_vmwait(ops_after(tq, t));
       if (BXF && t == t0) {   // the first tile's raw rows: transform them before everything
         lds_barrier();
         transform(le1, t0);
       }
       lds_barrier();
       if (t > t0) store_c(t - 1);
-      dma(clampt(t + D - 1));
+      if (!CTN_DU_LATE) {
+        if (!CTN_DU_NOCLAMP) dma(clampt(t + D - 1));
+        else if (t + D - 1 < t1) dma(t + D - 1);
+      }
       if constexpr (BXF) transform(le1, clampt(t + 1));
       compute(t, acc);
       if constexpr (CTN_DU_EXP & 32) __builtin_amdgcn_sched_barrier(0);
+      // cLN with DMA'd row statistics: no LDS-DMA in flight while the epilogue reads
+      // its LDS operands (the one configuration measured reproducible)
+      if constexpr (CST || (CTN_DU_DBG & 1)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       epilogue(le1, t, acc);
+      if (CTN_DU_LATE) {   // after the epilogue: its slot (t-1)%D was last read before this phase's barrier
+        if (!CTN_DU_NOCLAMP) dma(clampt(t + D - 1));
+        else if (t + D - 1 < t1) dma(t + D - 1);
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may land after the workgroup ends
     lds_barrier();

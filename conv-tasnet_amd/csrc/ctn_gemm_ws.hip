@@ -369,7 +369,9 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
   // per-lane fp64 partials of the current utterance run, reduced over the wave and
   // stored once per run
   auto flush_run = [&]() __attribute__((always_inline)) {
-    const double s = wave_sum(run_s), q = wave_sum(run_q);
+    // DPP, not ds_bpermute: no LDS-unit cross-lane traffic while LDS-DMA is in flight
+    // (dual-GEMM reproducibility)
+    const double s = wave_sum_dpp_d(run_s), q = wave_sum_dpp_d(run_q);
     if (lane == 0) p.grp_slab[((size_t)rr * (S * WV) + wslot) * kmax + (run_m - m0)] = make_double2(s, q);
   };
 
@@ -449,9 +451,7 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
         } else {
           // per-row partial over this wave's 16*NB channels: reduce across the 4 lane
           // groups; all four groups store the same value (no divergent store)
-          float s = s2[0] + s2[1], ss = q2[0] + q2[1];
-          s += __shfl_xor(s, 16, 64); ss += __shfl_xor(ss, 16, 64);
-          s += __shfl_xor(s, 32, 64); ss += __shfl_xor(ss, 32, 64);
+          const float s = xsum_rows(s2[0] + s2[1]), ss = xsum_rows(q2[0] + q2[1]);   // VALU swaps
           if (CLN_FIN && p.stats_out) {
             if (lg == 0) scln[((t & 1) * TM + mb * 16 + lr) * WV + wid] = make_double2((double)s, (double)ss);
           } else {
@@ -543,9 +543,12 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
       // fragment image holds row mb*16 + (x ^ (lg + 4(kb&3))), k-chunk 4kb + lg, the
       // ws_slot layout.  Per tile: wait for this wave's DMA of tile t (counted: the DMA
       // instructions of the later tiles and the output stores issued since may stay in
-      // flight; optional stores only make the wait stricter), barrier, DMA of tile
+      // flight), barrier, DMA of tile
       // t+WS_DR-1 into the slot tile t-1 was read from, MFMAs, epilogue, stores.
-      constexpr int NF = MB * KB, NFW = NF / WV, SPT = MB * Q;
+      // The count assumes exactly SPT output stores per tile after each tile's DMA:
+      // more (cln_final) only make the wait stricter, fewer would make it too loose,
+      // so the store-free bound-finding build (CTN_WS_EXP bit 0) counts none.
+      constexpr int NF = MB * KB, NFW = NF / WV, SPT = (CTN_WS_EXP & 1) ? 0 : MB * Q;
       static_assert(NF % WV == 0, "whole fragments per wave");
       static_assert(NFW * (WS_DR - 2) + SPT * (WS_DR - 1) <= 23, "vmcnt range of vmwait23");
       uint32_t voff[NFW];

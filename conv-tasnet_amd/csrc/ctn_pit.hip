@@ -10,6 +10,12 @@
 // pit_reorder: masked estimate in place + reorder by the winning permutation,
 //             keeping the reference's perm-not-inverse indexing (:91-97).
 // pit_bwd   : dL/dest[m][i][t] = scale_m (alpha s_j[t] + beta e_i[t] + offset), t < length.
+//
+// C <= 4: pit_final is one workgroup, one thread per utterance, the C! <= 24
+// permutations from a table in the kernel arguments.  5 <= C <= 8 (C! up to 40,320):
+// pit_final_wide runs one workgroup per utterance whose threads split the
+// permutation indices (each decoded from its lexicographic rank, the order of
+// itertools.permutations), then pit_loss sums the utterances' maxima.
 #include "ctn_codec.h"
 #include "ctn_common.h"
 
@@ -133,6 +139,106 @@ __global__ __launch_bounds__(256) void pit_final_kernel(PitArgs a) {
   if (threadIdx.x == 0) a.loss[0] = (float)(-l1[0] / a.M);
 }
 
+// permutation of range(C) with lexicographic rank p (itertools.permutations order)
+CTN_DEV void pit_decode(long p, int C, int* out) {
+  long f = 1;
+  for (int i = 2; i < C; ++i) f *= i;   // (C-1)!
+  unsigned used = 0;
+  for (int i = 0; i < C; ++i) {
+    const int d = (int)(p / f);
+    p %= f;
+    if (C - 1 - i > 0) f /= C - 1 - i;
+    int v = 0;
+    for (int cnt = -1; v < C; ++v)
+      if (!((used >> v) & 1u) && ++cnt == d) break;
+    used |= 1u << v;
+    out[i] = v;
+  }
+}
+
+// 5 <= C <= 8: one workgroup per utterance (pit_criterion.py:41-75 for one row)
+template <int C>
+__global__ __launch_bounds__(256) void pit_final_wide_kernel(PitArgs a) {
+  constexpr int NV = 5 * C + C * C;
+  __shared__ double v[NV], snr[C][C], ratio[C][C], Pp[C][C], Ne[C][C], Dm[C][C], Et[C], eb[C];
+  __shared__ double bv[256];
+  __shared__ long bp[256];
+  const int m = blockIdx.x, tid = threadIdx.x;
+  for (int i = tid; i < NV; i += 256) {   // chunk partials in chunk order, as pit_final
+    double s = 0.0;
+    for (int ch = 0; ch < a.chunks; ++ch) s += a.slab[((size_t)m * a.chunks + ch) * NV + i];
+    v[i] = s;
+  }
+  __syncthreads();
+  const double n = (double)a.lengths[m];
+  if (tid < C * C) {
+    const int i = tid / C, j = tid % C;
+    const double ebi = v[i] / n, sbj = v[2 * C + j] / n;
+    const double Ee = v[3 * C + i] - 2.0 * ebi * v[i] + n * ebi * ebi;
+    const double Etj = v[4 * C + j] - 2.0 * sbj * v[C + j] + n * sbj * sbj;
+    const double D = v[5 * C + i * C + j] - ebi * v[C + j] - sbj * v[i] + n * ebi * sbj;
+    const double E = Etj + PIT_EPS;
+    Pp[i][j] = D * D * Etj / (E * E);
+    Ne[i][j] = Ee - 2.0 * D * D / E + D * D * Etj / (E * E);
+    ratio[i][j] = Pp[i][j] / (Ne[i][j] + PIT_EPS);
+    snr[i][j] = 10.0 * log10(ratio[i][j] + PIT_EPS);
+    Dm[i][j] = D;
+    if (i == 0) Et[j] = Etj;
+    if (j == 0) eb[i] = ebi;
+  }
+  __syncthreads();
+  long nperm = 1;
+  for (int i = 2; i <= C; ++i) nperm *= i;
+  double best = -1e300;
+  long bi = nperm;
+  for (long p = tid; p < nperm; p += 256) {
+    int pm[C];
+    pit_decode(p, C, pm);
+    double sv = 0.0;
+#pragma unroll
+    for (int i = 0; i < C; ++i) sv += snr[i][pm[i]];
+    if (sv > best) { best = sv; bi = p; }   // ascending p: first maximum of this thread
+  }
+  bv[tid] = best;
+  bp[tid] = bi;
+  __syncthreads();
+  if (tid == 0) {
+    for (int t = 1; t < 256; ++t)   // first maximum over all ranks, like torch.argmax
+      if (bv[t] > best || (bv[t] == best && bp[t] < bi)) { best = bv[t]; bi = bp[t]; }
+    const double ms = best / C;
+    a.max_snr[m] = (float)ms;
+    a.best[m] = bi;
+    a.msd[m] = ms;
+    int pm[C];
+    pit_decode(bi, C, pm);
+    for (int i = 0; i < C; ++i) {
+      const int j = pm[i];
+      const double E = Et[j] + PIT_EPS, Nd = Ne[i][j] + PIT_EPS, D = Dm[i][j];
+      const double dsnr = 10.0 / (log(10.0) * (ratio[i][j] + PIT_EPS));
+      const double dPp = 2.0 * D * Et[j] / (E * E);
+      const double dNe = -4.0 * D / E + 2.0 * D * Et[j] / (E * E);
+      const double dr_dD = (dPp * Nd - Pp[i][j] * dNe) / (Nd * Nd);
+      const double dr_dEe = -Pp[i][j] / (Nd * Nd);
+      const double al = dsnr * dr_dD / C, be = 2.0 * dsnr * dr_dEe / C;
+      const double off = -al * v[C + j] / n - be * eb[i];
+      float* cf = a.coef + ((size_t)m * C + i) * 4;
+      cf[0] = (float)al;
+      cf[1] = (float)be;
+      cf[2] = (float)off;
+      cf[3] = (float)j;
+    }
+  }
+}
+
+// loss = -mean over utterances of max_snr (pit_criterion.py:22), the summation order of pit_final
+__global__ __launch_bounds__(256) void pit_loss_kernel(PitArgs a) {
+  __shared__ double red[4];
+  double l1[1] = {0.0};
+  for (int m = threadIdx.x; m < a.M; m += 256) l1[0] += a.msd[m];
+  block_sum_d<1>(l1, red);
+  if (threadIdx.x == 0) a.loss[0] = (float)(-l1[0] / a.M);
+}
+
 template <int C>
 __global__ __launch_bounds__(256) void pit_reorder_kernel(PitArgs a) {
   const long total = (long)a.M * a.T;
@@ -146,7 +252,8 @@ __global__ __launch_bounds__(256) void pit_reorder_kernel(PitArgs a) {
       const int b = (int)a.best[m];
 #pragma unroll
       for (int c = 0; c < C; ++c) {
-        const int pc = a.perms[b][c];   // reorder_source[b, c] = source[b, perm[c]] (pit_criterion.py:97)
+        // reorder_source[b, c] = source[b, perm[c]] (pit_criterion.py:97)
+        const int pc = C <= 4 ? a.perms[b][c] : (int)a.coef[((size_t)m * C + c) * 4 + 3];
         float val = e[0];
 #pragma unroll
         for (int q = 1; q < C; ++q) val = pc == q ? e[q] : val;
@@ -182,7 +289,13 @@ __global__ __launch_bounds__(256) void pit_bwd_kernel(PitArgs a) {
 template <int C>
 static hipError_t pit_fwd_c(const PitArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(pit_stats_kernel<C>, dim3(a.chunks, a.M), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(pit_final_kernel<C>, dim3(1), dim3(256), 0, s, a);
+  if constexpr (C <= 4) {
+    hipLaunchKernelGGL(pit_final_kernel<C>, dim3(1), dim3(256), 0, s, a);
+  } else {
+    if (!a.msd) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(pit_final_wide_kernel<C>, dim3(a.M), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(pit_loss_kernel, dim3(1), dim3(256), 0, s, a);
+  }
   long total = (long)a.M * a.T;
   int g = (int)((total + 255) / 256);
   if (g > 2048) g = 2048;
@@ -205,6 +318,10 @@ hipError_t launch_pit_forward(const PitArgs& a, hipStream_t s) {
     case 2: return pit_fwd_c<2>(a, s);
     case 3: return pit_fwd_c<3>(a, s);
     case 4: return pit_fwd_c<4>(a, s);
+    case 5: return pit_fwd_c<5>(a, s);
+    case 6: return pit_fwd_c<6>(a, s);
+    case 7: return pit_fwd_c<7>(a, s);
+    case 8: return pit_fwd_c<8>(a, s);
   }
   return hipErrorInvalidValue;
 }
@@ -215,6 +332,10 @@ hipError_t launch_pit_backward(const PitArgs& a, hipStream_t s) {
     case 2: return pit_bwd_c<2>(a, s);
     case 3: return pit_bwd_c<3>(a, s);
     case 4: return pit_bwd_c<4>(a, s);
+    case 5: return pit_bwd_c<5>(a, s);
+    case 6: return pit_bwd_c<6>(a, s);
+    case 7: return pit_bwd_c<7>(a, s);
+    case 8: return pit_bwd_c<8>(a, s);
   }
   return hipErrorInvalidValue;
 }

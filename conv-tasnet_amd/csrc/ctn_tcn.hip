@@ -183,10 +183,12 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
   };
   auto finish = [&](const Raw8<T>& r, bool ok, float2 st, f32x2_t* out) {
     const f32x2_t nm = {-st.x, -st.x};
-    const float okf = ok ? 1.f : 0.f;   // rows outside the utterance: 0 (their inputs are finite)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      out[i] = pfma((pr2(f32x2_t{r[2 * i], r[2 * i + 1]}, al1) + nm) * st.y, g1[i], b1[i]) * okf;
+    for (int i = 0; i < 4; ++i) {   // rows outside the utterance: exactly 0 (a select, so a
+                                    // non-finite value in the row it fetched cannot leak in)
+      const f32x2_t v = pfma((pr2(f32x2_t{r[2 * i], r[2 * i + 1]}, al1) + nm) * st.y, g1[i], b1[i]);
+      out[i] = f32x2_t{ok ? v[0] : 0.f, ok ? v[1] : 0.f};
+    }
   };
 #pragma unroll
   for (int i = 0; i < P - 1; ++i) {           // prologue: steps j0-POWN .. j0+P-2-POWN
@@ -363,7 +365,6 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
     const float2 st = NK == NORM_GLN ? st2u : a.st2[row];
     const float2 sm = NK == NORM_GLN ? sm2u : a.sm2[row];
     const f32x2_t nm = {-st.x, -st.x}, nsx = {-sm.x, -sm.x}, nsy = {-sm.y, -sm.y};
-    const float okf = ok ? 1.f : 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const f32x2_t x = {rd[2 * i], rd[2 * i + 1]};
@@ -371,7 +372,8 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
       const f32x2_t gn = {rg[2 * i], rg[2 * i + 1]};                     // dL/d(norm2 output)
       const f32x2_t ga = pfma(ah, nsy, pfma(gn, g2[i], nsx)) * st.y;     // dL/da2
       const f32x2_t dx = {x[0] > 0.f ? 1.f : al2, x[1] > 0.f ? 1.f : al2};
-      gd[i] = (ga * dx) * okf;   // rows outside the utterance: 0 (their inputs are finite)
+      const f32x2_t g = ga * dx;
+      gd[i] = f32x2_t{ok ? g[0] : 0.f, ok ? g[1] : 0.f};   // rows outside the utterance: exactly 0
       if (ok && count) {
         calpha = fmaf(ga[0], x[0] > 0.f ? 0.f : x[0], calpha);   // channel order
         calpha = fmaf(ga[1], x[1] > 0.f ? 0.f : x[1], calpha);

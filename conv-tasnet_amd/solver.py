@@ -208,8 +208,10 @@ class Solver(object):
         for i, batch in enumerate(loader):
             mixture, lengths, source = self._batch_to_device(batch, dev)
             if cross_valid:
+                # the unwrapped module: a DDP forward would broadcast buffers (BN running
+                # stats), a collective that ranks without a cv minibatch never join
                 with torch.no_grad():
-                    loss = cal_loss(source, self.model(mixture), lengths)[0]
+                    loss = cal_loss(source, _inner(self.model)(mixture), lengths)[0]
             else:
                 loss = cal_loss(source, self.model(mixture), lengths)[0]
                 self.optimizer.zero_grad()

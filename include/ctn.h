@@ -164,6 +164,8 @@ int ctn_decoder_backward(const ctn_codec_desc* d, const void* x_last, const void
  * get_mask, src/pit_criterion.py:12-113.  `est` is masked in place beyond
  * each length (:37-38); `reordered` (nullable) keeps the reference's
  * perm-not-inverse indexing (:91-97).  `coef` [M*C*4] is saved for backward.
+ * 1 <= C <= 8 (all C! permutations, :66; 0 workspace bytes / CTN_ERR_UNSUPPORTED
+ * beyond); the encoder/decoder descriptors accept the same range.
  * ------------------------------------------------------------------------- */
 typedef struct { int32_t M, C, T; } ctn_pit_desc;
 size_t ctn_pit_workspace_bytes(const ctn_pit_desc* d);

@@ -1,0 +1,46 @@
+"""Golden vectors for more than 4 speakers, captured from the REAL reference (build
+container only; the same import shim as make_golden.py, whose helpers this reuses).
+
+Run from the repo root:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_wide.py
+
+pit_wide.npz   : cal_loss (pit_criterion.py:12-113) for C = 5, 6, 8 — C! = 120, 720,
+                 40,320 permutations (pit_criterion.py:66) — equal and unequal lengths
+model_5spk.npz : a full ConvTasNet forward + PIT loss + backward at C = 5 (small dims)
+"""
+import numpy as np
+import torch
+
+import make_golden as mg
+from oracle import ctn_oracle as O
+
+
+def pit_wide_fixtures():
+    rng = np.random.default_rng(310)
+    out = {}
+    for C, T in ((5, 1000), (6, 700), (8, 400)):
+        for tag, lens in (("eq", [T, T]), ("neq", [T, T * 2 // 3])):
+            src = rng.standard_normal((2, C, T)).astype(np.float32)
+            for b, l in enumerate(lens):
+                src[b, :, l:] = 0
+            perm = [list(rng.permutation(C)) for _ in range(2)]
+            est = np.stack([src[b, perm[b]] for b in range(2)]) * 0.8 + \
+                0.5 * rng.standard_normal((2, C, T)).astype(np.float32) + 0.3
+            s = torch.from_numpy(src)
+            e = torch.from_numpy(est.astype(np.float32)).requires_grad_(True)
+            e2 = e * 1.0
+            lengths = torch.tensor(lens)
+            loss, max_snr, est_m, reord = mg.ref_pit.cal_loss(s, e2, lengths)
+            loss.backward()
+            k = f"pit.C{C}.{tag}"
+            out.update({k + ".src": s, k + ".est": e.detach(), k + ".len": lengths,
+                        k + ".loss": loss.detach(), k + ".max_snr": max_snr.detach(),
+                        k + ".est_m": est_m.detach(), k + ".reord": reord.detach(),
+                        k + ".gest": e.grad, k + ".perm": np.array(perm)})
+    mg.save("pit_wide.npz", **out)
+
+
+if __name__ == "__main__":
+    torch.manual_seed(0)
+    pit_wide_fixtures()
+    mg.model_fixture("model_5spk.npz", O.Cfg(64, 20, 64, 128, 3, 2, 2, 5), 2, 4000, 6,
+                     lens=[4000, 3300], full=True)

@@ -83,8 +83,10 @@ def test_forward_rejects_null_and_small_workspace(lib):
     sv = L.TBlockSaved()
     assert lib.ctn_tblock_forward(ctypes.byref(d), ctypes.byref(p), None, None, ctypes.byref(sv), None, 0, None) == 1
     assert lib.ctn_pit_forward(None, None, None, None, None, None, None, None, None, None, 0, None) == 1
-    pd = L.PitDesc(2, 5, 100)
-    assert lib.ctn_pit_workspace_bytes(ctypes.byref(pd)) == 0          # C > 4 unsupported
+    pd = L.PitDesc(2, 9, 100)
+    assert lib.ctn_pit_workspace_bytes(ctypes.byref(pd)) == 0          # C > 8 unsupported
+    pd = L.PitDesc(2, 8, 100)
+    assert lib.ctn_pit_workspace_bytes(ctypes.byref(pd)) > 0           # C! = 40,320 permutations
 
 
 def test_codec_validation(lib):

@@ -59,7 +59,7 @@ def run(model, g, bf16=False):
 
 
 MODELS = ["model_c1.npz", "model_paper_short.npz", "model_causal_cln.npz", "model_3spk.npz",
-          "model_softmax_pad.npz", "model_bn.npz"]
+          "model_softmax_pad.npz", "model_bn.npz", "model_5spk.npz"]
 
 
 @pytest.mark.parametrize("name", MODELS)
@@ -212,11 +212,13 @@ def test_decoder_standalone(L_):
                                atol=1e-3)
 
 
-@pytest.mark.parametrize("C", [2, 3])
+@pytest.mark.parametrize("C", [2, 3, 5, 6, 8])
 @pytest.mark.parametrize("tag", ["eq", "neq"])
 def test_pit_loss(C, tag):
+    """C <= 3: pit.npz; C = 5, 6, 8 (C! up to 40,320 permutations, the device-decoded
+    wide path): pit_wide.npz (tests/golden/make_golden_wide.py)."""
     import pit_criterion as pc
-    g = load("pit.npz")
+    g = load("pit.npz" if C <= 3 else "pit_wide.npz")
     k = f"pit.C{C}.{tag}"
     est0 = T(g[k + ".est"]).requires_grad_(True)
     est = est0 * 1.0

@@ -92,10 +92,10 @@ def test_temporal_block(norm, causal, d):
         close(params[pre + n].grad, g[tag + ".g:" + n], 1e-4, 2e-4)
 
 
-@pytest.mark.parametrize("C", [2, 3])
+@pytest.mark.parametrize("C", [2, 3, 5, 6, 8])
 @pytest.mark.parametrize("tag", ["eq", "neq"])
 def test_pit(C, tag):
-    g = load("pit.npz")
+    g = load("pit.npz" if C <= 3 else "pit_wide.npz")   # pit_wide: make_golden_wide.py
     k = f"pit.C{C}.{tag}"
     est = T(g[k + ".est"]).clone().requires_grad_(True)
     loss, max_snr, est_m, reord = O.cal_loss(T(g[k + ".src"]), est, T(g[k + ".len"]))
@@ -127,7 +127,7 @@ def model_params(g, cfg):
 
 
 MODELS = ["model_c1.npz", "model_paper_short.npz", "model_causal_cln.npz", "model_3spk.npz",
-          "model_softmax_pad.npz", "model_bn.npz"]
+          "model_softmax_pad.npz", "model_bn.npz", "model_5spk.npz"]
 
 
 @pytest.mark.parametrize("name", MODELS)

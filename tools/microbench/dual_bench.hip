@@ -8,6 +8,9 @@
 #include "../../conv-tasnet_amd/csrc/ctn_gemm_dual.hip"
 
 using namespace ctn;
+#ifndef DB_CLN
+#define DB_CLN 0   // 1: pair A with per-row (cLN) statistics
+#endif
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 
@@ -49,10 +52,10 @@ int main() {
   struct Case { const char* name; GemmDual g; double bytes; };
   std::vector<Case> cs;
   {
-    GemmDual g{}; g.g = Rows{M, K, Kp}; g.Kred = B; g.Nout = H; g.norm = NORM_GLN;
+    GemmDual g{}; g.g = Rows{M, K, Kp}; g.Kred = B; g.Nout = H; g.norm = DB_CLN ? NORM_CLN : NORM_GLN;
     g.A = gy; g.lda = B; g.W = w; g.ldw = B; g.C = out; g.ldc = H; g.epi = EPI_NORM_BWD; g.R = d; g.ldr = H;
     g.alpha = al; g.stats = (const float2*)st; g.gamma = gm; g.grp_slab = slab;
-    g.Bm = d; g.ldb = H; g.bop.kind = OP_PRELU_NORM; g.bop.norm = NORM_GLN; g.bop.stats = (const float2*)st;
+    g.Bm = d; g.ldb = H; g.bop.kind = OP_PRELU_NORM; g.bop.norm = g.norm; g.bop.stats = (const float2*)st;
     g.bop.gamma = gm; g.bop.beta = bt; g.bop.alpha = al; g.Dpart = dpart;
     cs.push_back({"A: gy.W2t norm-bwd + dW2", g, rows * (B + 2 * H) * 2.0});
   }

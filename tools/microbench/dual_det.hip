@@ -3,6 +3,7 @@
 // slab) differ from the first launch.  Diagnostic only; not part of the library.
 #include <stdio.h>
 #include <stdlib.h>
+#include <math.h>
 #include <string.h>
 #include <algorithm>
 #include <vector>
@@ -82,6 +83,33 @@ int main(int argc, char** argv) {
       auto c = get<uint16_t>(out, cn);
       auto dd = get<float>(dpart, nd);
       auto ss = get<double2>(slab, nslab);
+      if (pair == 0 && NK == NORM_CLN) {   // the per-row (sum ga, sum ga*ahat) entries against a host
+        // recomputation from the bf16 C rows (approximate: the kernel sums fp32 accumulators)
+        static std::vector<uint16_t> hd;
+        if (hd.empty()) hd = get<uint16_t>(d, rows * H);
+        auto bf = [](uint16_t v) { uint32_t u = (uint32_t)v << 16; float f; memcpy(&f, &u, 4); return f; };
+        long nbad = 0, shown = 0;
+        for (long row = 0; row < rows; ++row) {
+          if (row % Kp >= K) continue;
+          for (int e = 0; e < 16; ++e) {
+            double hs = 0, hq = 0;
+            for (int ch = e * 32; ch < e * 32 + 32; ++ch) {
+              const float ga = bf(c[row * H + ch]);
+              float x = bf(hd[row * H + ch]);
+              x = x > 0.f ? x : 0.25f * x;
+              hs += ga;
+              hq += (double)ga * ((x - 0.1f) * 1.3f);
+            }
+            const double2 v = ss[row * 16 + e];
+            const double tol = 0.02 * (fabs(hq) + fabs(hs)) + 0.05;
+            if (fabs(v.x - hs) > tol || fabs(v.y - hq) > tol) {
+              ++nbad;
+              if (shown++ < 3) printf("   host check row %ld entry %d: kernel (%.6g, %.6g) host (%.6g, %.6g)\n", row, e, v.x, v.y, hs, hq);
+            }
+          }
+        }
+        printf("   run %d: %ld statistics entries off the host recomputation\n", r, nbad);
+      }
       if (r == 0) { c0 = c; d0 = dd; s0 = ss; continue; }
       long nc = 0, ndd = 0, ns = 0, first_c = -1, first_d = -1, first_s = -1;
       std::vector<int> rowhist(32, 0), colhist(16, 0);
@@ -122,6 +150,15 @@ int main(int argc, char** argv) {
         printf("\n   ... by (slice, wave column) entry:");
         for (int v : sl_nbg) printf(" %d", v);
         printf("\n");
+      }
+      if (ns && getenv("DET_VALUES")) {   // the first differing statistics entries, both runs
+        int shown = 0;
+        for (size_t i = 0; i < nslab && shown < 6; ++i)
+          if (memcmp(&ss[i], &s0[i], sizeof(double2))) {
+            printf("   slab[%zu] (row %zu, entry %zu): run0 (%.9g, %.9g) now (%.9g, %.9g)\n", i, i / 16, i % 16,
+                   s0[i].x, s0[i].y, ss[i].x, ss[i].y);
+            ++shown;
+          }
       }
       if (nc || ndd || ns) {
         ++bad;
