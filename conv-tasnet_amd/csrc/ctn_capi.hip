@@ -1522,3 +1522,75 @@ extern "C" int ctn_mask_backward(const ctn_rows_desc* d, int nspk, int mask_type
   CTN_HIP(launch_layer(dtype_of(d), LAYER_MASK_BWD, a, (hipStream_t)stream));
   return CTN_OK;
 }
+
+// ===========================================================================
+// Streaming causal separation (ctn_stream.hip)
+// ===========================================================================
+namespace {
+int stream_check(const ctn_stream_desc* d) {
+  if (!d) return fail(CTN_ERR_ARG, "null descriptor");
+  if (d->M < 1 || d->K < 1) return fail(CTN_ERR_ARG, "M=%d K=%d", d->M, d->K);
+  if (d->L < 2 || d->L % 2 || d->L > 64) return fail(CTN_ERR_UNSUPPORTED, "L=%d (even, <= 64)", d->L);
+  if (d->N < 1 || d->B < 1 || d->H < 1 || d->P < 1 || d->P > 8 || d->C < 1 || d->C > 8)
+    return fail(CTN_ERR_ARG, "N=%d B=%d H=%d P=%d C=%d", d->N, d->B, d->H, d->P, d->C);
+  if (d->norm != CTN_NORM_CLN && d->norm != CTN_NORM_BN)
+    return fail(CTN_ERR_UNSUPPORTED, "norm %d: gLN normalizes over the whole utterance and cannot stream", d->norm);
+  if (d->mask_type < 0 || d->mask_type > 2) return fail(CTN_ERR_ARG, "mask type %d", d->mask_type);
+  return CTN_OK;
+}
+StreamArgs stream_args(const ctn_stream_desc* d) {
+  StreamArgs a{};
+  a.M = d->M; a.K = d->K; a.N = d->N; a.L = d->L; a.B = d->B; a.H = d->H; a.P = d->P; a.C = d->C;
+  a.norm = d->norm == CTN_NORM_CLN ? 1 : 2;
+  a.mask_type = d->mask_type;
+  return a;
+}
+}  // namespace
+
+extern "C" int ctn_stream_encode(const ctn_stream_desc* d, const float* samples, int64_t ld_samples, const float* U,
+                                 const float* gamma0, const float* beta0, const float* wb_t, float* w_out,
+                                 float* x_out, void* stream) {
+  if (int rc = stream_check(d)) return rc;
+  if (!samples || !U || !gamma0 || !beta0 || !wb_t || !w_out || !x_out) return fail(CTN_ERR_ARG, "null pointer");
+  if (ld_samples < (int64_t)(d->K - 1) * (d->L / 2) + d->L) return fail(CTN_ERR_ARG, "ld_samples too small");
+  StreamArgs a = stream_args(d);
+  a.samples = samples; a.ld_samples = ld_samples; a.U = U; a.na = gamma0; a.nb = beta0; a.W = wb_t;
+  a.w_out = w_out; a.x_out = x_out;
+  CTN_HIP(launch_stream(0, a, (hipStream_t)stream));
+  return CTN_OK;
+}
+
+extern "C" int ctn_stream_block(const ctn_stream_desc* d, int dilation, int64_t pos, int ring_frames,
+                                const float* x_in, const float* w1_t, const float* alpha1, const float* norm1_a,
+                                const float* norm1_b, const float* wd, const float* alpha2, const float* norm2_a,
+                                const float* norm2_b, const float* w2_t, float* ring, float* x_out, void* stream) {
+  if (int rc = stream_check(d)) return rc;
+  if (dilation < 1 || pos < 0) return fail(CTN_ERR_ARG, "dilation %d, pos %lld", dilation, (long long)pos);
+  if (ring_frames < 1 || (ring_frames & (ring_frames - 1)) || ring_frames < (d->P - 1) * dilation + d->K)
+    return fail(CTN_ERR_ARG, "ring_frames %d: a power of two >= (P-1)*dilation + K = %d", ring_frames,
+                (d->P - 1) * dilation + d->K);
+  if (!x_in || !w1_t || !alpha1 || !norm1_a || !norm1_b || !wd || !alpha2 || !norm2_a || !norm2_b || !w2_t || !ring ||
+      !x_out)
+    return fail(CTN_ERR_ARG, "null pointer");
+  if (x_in == x_out) return fail(CTN_ERR_ARG, "x_out must not alias x_in (the residual is read per frame)");
+  StreamArgs a = stream_args(d);
+  a.dil = dilation; a.pos = pos; a.R = ring_frames; a.x_in = x_in; a.ring = ring;
+  a.W = w1_t; a.alpha1 = alpha1; a.na = norm1_a; a.nb = norm1_b;
+  CTN_HIP(launch_stream(1, a, (hipStream_t)stream));
+  a.W = w2_t; a.alpha2 = alpha2; a.na = norm2_a; a.nb = norm2_b; a.wd = wd; a.x_out = x_out;
+  CTN_HIP(launch_stream(2, a, (hipStream_t)stream));
+  return CTN_OK;
+}
+
+extern "C" int ctn_stream_decode(const ctn_stream_desc* d, const float* x_last, const float* w, const float* wm_t,
+                                 const float* V, const float* tail_in, float* tail_out, float* frames_ws, float* out,
+                                 void* stream) {
+  if (int rc = stream_check(d)) return rc;
+  if (!x_last || !w || !wm_t || !V || !tail_in || !tail_out || !frames_ws || !out) return fail(CTN_ERR_ARG, "null pointer");
+  if (tail_in == tail_out) return fail(CTN_ERR_ARG, "tail_out must not alias tail_in");
+  StreamArgs a = stream_args(d);
+  a.x_in = x_last; a.w_in = w; a.W = wm_t; a.V = V; a.tail_in = tail_in; a.tail_out = tail_out;
+  a.frames = frames_ws; a.out = out;
+  CTN_HIP(launch_stream(3, a, (hipStream_t)stream));
+  return CTN_OK;
+}

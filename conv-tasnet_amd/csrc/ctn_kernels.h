@@ -276,4 +276,31 @@ hipError_t launch_grad_clip(const OptSegment* segs, const OptChunk* chunks, int 
 hipError_t launch_adam(const OptSegment* segs, const OptChunk* chunks, int nchunks, const AdamArgs& a,
                        hipStream_t s);
 
+// ---- streaming causal separation (ctn_stream.hip) ----------------------------------
+struct StreamArgs {
+  int M, K, N, L, B, H, P, C, norm, mask_type, dil, R;
+  long pos, ld_samples;
+  const float* samples;          // encode: [M][ld_samples]
+  const float* U;                // encode: [N][L]
+  const float* na;               // norm: cLN gamma or affine scale [channels]
+  const float* nb;               // norm: cLN beta or affine shift
+  const float* W;                // transposed 1x1 weight [in][out]
+  const float* alpha1;           // PReLU 1 (block_in)
+  const float* alpha2;           // PReLU 2 (block_out)
+  const float* wd;               // depthwise [H][P]
+  const float* x_in;             // [M][K][B]
+  const float* w_in;             // decode: encoder output [M][K][N]
+  const float* V;                // decode: basis [L][N]
+  const float* tail_in;          // decode: [M][C][L/2]
+  float* w_out;                  // encode: [M][K][N]
+  float* x_out;                  // [M][K][B]
+  float* ring;                   // [M][R][H]
+  float* frames;                 // decode scratch [M][C][K][L]
+  float* tail_out;               // [M][C][L/2]
+  float* out;                    // [M][C][K*L/2]
+};
+// which: 0 encode, 1 block in (1x1, PReLU, norm 1 -> ring), 2 block out (depthwise, PReLU,
+// norm 2, 1x1, residual), 3 decode (mask, sources, frames, overlap-add)
+hipError_t launch_stream(int which, const StreamArgs& a, hipStream_t s);
+
 }  // namespace ctn

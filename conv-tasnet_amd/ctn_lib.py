@@ -14,7 +14,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CTN_HIP_LIB", os.path.join(_HERE, "libctn_hip.so"))
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 DTYPE_F32, DTYPE_BF16 = 0, 1
 NORM_GLN, NORM_CLN, NORM_BN = 0, 1, 2
@@ -71,6 +71,10 @@ MASK_IDENTITY = 2
 
 class RowsDesc(ctypes.Structure):
     _fields_ = [(n, c_int32) for n in ("M", "K", "Kp", "C", "dtype")]
+
+
+class StreamDesc(ctypes.Structure):
+    _fields_ = [(n, c_int32) for n in ("M", "K", "N", "L", "B", "H", "P", "C", "norm", "mask_type")]
 
 
 class OptSegment(ctypes.Structure):
@@ -134,6 +138,10 @@ _SIGS = {
     "ctn_mask_forward": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p]),
     "ctn_mask_backward": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p,
                                          c_void_p]),
+    "ctn_stream_encode": (ctypes.c_int, [c_void_p, c_void_p, ctypes.c_int64] + [c_void_p] * 6 + [c_void_p]),
+    "ctn_stream_block": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int] + [c_void_p] * 12 +
+                         [c_void_p]),
+    "ctn_stream_decode": (ctypes.c_int, [c_void_p] + [c_void_p] * 8 + [c_void_p]),
     "ctn_timer_enable": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "ctn_timer_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
 }

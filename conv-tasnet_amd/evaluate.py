@@ -57,49 +57,58 @@ def reorder_inverse(est, source, lengths):
     return torch.gather(est, 1, inv.unsqueeze(-1).expand(-1, -1, est.size(-1)))
 
 
+class Evaluator:
+    """Scores a trained model over one manifest directory (src/evaluate.py:33-90 behaviour:
+    the same per-utterance printout and averages).  Minibatches are separated on the
+    device, scored there in fp64 (SI-SNRi, cal_SISNRi_batch) and, with --cal_sdr, on the
+    host (SDRi, cal_SDRi); ``records`` keeps one (SI-SNRi, SDRi or None) per utterance."""
+
+    def __init__(self, args):
+        self.args = args
+        self.model = ConvTasNet.load_model(args.model_path)
+        print(self.model)
+        self.model.eval().cuda()
+        dataset = AudioDataset(args.data_dir, args.batch_size, sample_rate=args.sample_rate, segment=-1)
+        self.loader = AudioDataLoader(dataset, batch_size=1, num_workers=args.num_workers)
+        self.records = []
+
+    def _separate(self, mixture, lengths, source):
+        """-> estimates paired with the targets (the reference's reorder, or --pit_fix)."""
+        est = self.model(mixture)                                   # [B, C, T]
+        _, _, est, paired = cal_loss(source, est, lengths)
+        if self.args.pit_fix:
+            paired = reorder_inverse(est, source, lengths)
+        return paired
+
+    def _score(self, mixture, lengths, source, paired):
+        sisnri = cal_SISNRi_batch(source, paired, mixture, lengths).cpu().tolist()
+        sdri = [None] * len(sisnri)
+        if self.args.cal_sdr:
+            mix_u, src_u, est_u = (remove_pad(t, lengths) for t in (mixture, source, paired))
+            sdri = [cal_SDRi(src_u[b], est_u[b], mix_u[b]) for b in range(len(sisnri))]
+        return list(zip(sisnri, sdri))
+
+    @torch.no_grad()
+    def run(self):
+        for mixture, lengths, source in self.loader:
+            mixture, lengths, source = mixture.cuda(), lengths.cuda(), source.cuda()
+            for si, sd in self._score(mixture, lengths, source, self._separate(mixture, lengths, source)):
+                self.records.append((si, sd))
+                print("Utt", len(self.records))
+                if sd is not None:
+                    print("\tSDRi={0:.2f}".format(sd))
+                print("\tSI-SNRi={0:.2f}".format(si))
+        n = len(self.records)
+        if self.args.cal_sdr:
+            print("Average SDR improvement: {0:.2f}".format(sum(r[1] for r in self.records) / n))
+        mean_sisnri = sum(r[0] for r in self.records) / n
+        print("Average SISNR improvement: {0:.2f}".format(mean_sisnri))
+        return mean_sisnri
+
+
 def evaluate(args):
-    total_SISNRi = 0
-    total_SDRi = 0
-    total_cnt = 0
-
-    model = ConvTasNet.load_model(args.model_path)
-    print(model)
-    model.eval()
-    model.cuda()
-
-    dataset = AudioDataset(args.data_dir, args.batch_size, sample_rate=args.sample_rate, segment=-1)
-    data_loader = AudioDataLoader(dataset, batch_size=1, num_workers=args.num_workers)
-
-    with torch.no_grad():
-        for i, (data) in enumerate(data_loader):
-            padded_mixture, mixture_lengths, padded_source = data
-            padded_mixture = padded_mixture.cuda()
-            mixture_lengths = mixture_lengths.cuda()
-            padded_source = padded_source.cuda()
-            estimate_source = model(padded_mixture)  # [B, C, T]
-            loss, max_snr, estimate_source, reorder_estimate_source = \
-                cal_loss(padded_source, estimate_source, mixture_lengths)
-            if args.pit_fix:
-                reorder_estimate_source = reorder_inverse(estimate_source, padded_source, mixture_lengths)
-            sisnri = cal_SISNRi_batch(padded_source, reorder_estimate_source, padded_mixture,
-                                      mixture_lengths).cpu().tolist()
-            if args.cal_sdr:
-                mixture = remove_pad(padded_mixture, mixture_lengths)
-                source = remove_pad(padded_source, mixture_lengths)
-                est = remove_pad(reorder_estimate_source, mixture_lengths)
-            for b, avg_SISNRi in enumerate(sisnri):
-                print("Utt", total_cnt + 1)
-                if args.cal_sdr:
-                    avg_SDRi = cal_SDRi(source[b], est[b], mixture[b])
-                    total_SDRi += avg_SDRi
-                    print("\tSDRi={0:.2f}".format(avg_SDRi))
-                print("\tSI-SNRi={0:.2f}".format(avg_SISNRi))
-                total_SISNRi += avg_SISNRi
-                total_cnt += 1
-    if args.cal_sdr:
-        print("Average SDR improvement: {0:.2f}".format(total_SDRi / total_cnt))
-    print("Average SISNR improvement: {0:.2f}".format(total_SISNRi / total_cnt))
-    return total_SISNRi / total_cnt
+    """src/evaluate.py:33's entry point: score the model, return the mean SI-SNRi."""
+    return Evaluator(args).run()
 
 
 def cal_SDRi(src_ref, src_est, mix):

@@ -1,38 +1,52 @@
-"""Streaming (chunk-by-chunk) separation with a causal Conv-TasNet (SURVEY.md
-§8f row 4, stretch item): audio arrives in chunks of any length, separated
-audio leaves with a fixed delay of one encoder stride, and the concatenated
-output equals ``ConvTasNet.forward`` on the whole signal.
+"""Streaming (chunk-by-chunk) separation with a causal Conv-TasNet (SURVEY.md §8f
+row 4): audio arrives in chunks of any length, separated audio leaves with a fixed
+delay of one encoder stride, and the concatenated output equals
+``ConvTasNet.forward`` on the whole signal (the reference's separate.py:35-79 run
+on a causal model, conv_tasnet.py:176, 251-260, 289).
 
-Why a causal model streams (conv_tasnet.py:176, 251-260, 289): with
-``causal=True`` every operation is either per frame (encoder, cLN, 1x1 convs,
-PReLU, mask and its nonlinearity, decoder basis) or looks only BACKWARD in time
-(the dilated depthwise conv after Chomp1d reaches (P-1)*d frames into the
-past).  gLN normalizes over the whole utterance and cannot stream; BatchNorm
-streams in eval mode (running statistics, per frame).
+Why a causal model streams: with ``causal=True`` every operation is either per
+frame (encoder, cLN, 1x1 convs, PReLU, mask and its nonlinearity, decoder basis)
+or looks only BACKWARD in time (the dilated depthwise conv after Chomp1d reaches
+(P-1)*d frames into the past).  gLN normalizes over the whole utterance and
+cannot stream; BatchNorm streams in eval mode (running statistics, per frame).
 
-State kept between chunks (all on the device):
-* ``samples``: input samples not yet consumed by a whole encoder frame
-  (< L; frame k covers samples [k*L/2, k*L/2 + L));
-* per TemporalBlock, a ring of its last (P-1)*d INPUT frames — the block is
-  re-run on [history | new frames] and only the new frames are kept, so the
-  depthwise taps of every new frame see exactly the frames the full forward
-  gives them, and the kernel's causal zero padding stands in for the frames
-  before the start of the stream (history shorter than (P-1)*d);
-* ``tail``: the last L/2 output samples of the previous chunk's overlap-add,
-  which the next chunk's first frame completes.
+State kept between chunks (all on the device, fp32), nothing re-run:
+* ``samples``: input samples not yet consumed by a whole encoder frame;
+* per TemporalBlock a RING of its depthwise-conv input frames (after conv1x1,
+  PReLU and norm 1): a new frame is computed once, written to slot g % R, and
+  read by the depthwise taps of the frames g .. g + (P-1)*d; taps before the
+  stream start read as zero (the reference's causal zero padding);
+* ``tail``: the last L/2 overlap-add samples of the previous chunk.
 
-Each chunk runs the same native calls as the model forward (EncoderFn,
-TBlockFn per block, DecoderFn: include/ctn.h) on the chunk's frames plus the
-block histories; rows are re-laid out per block with torch copies.  Forward
-only (torch.no_grad).
+Per chunk of K new frames (cut into calls of at most ``max_frames``): one
+encode call, two kernels per TemporalBlock, one decode call (include/ctn.h
+``ctn_stream_*``, csrc/ctn_stream.hip) — work proportional to the NEW frames
+only, no padding of a call to 128-frame tiles.  Forward only (torch.no_grad);
+the weights are snapshotted (transposed 1x1 weights, folded BatchNorm) when the
+streamer is built or ``refresh_weights()`` is called.
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
+import torch.nn as nn
 
 import ctn_lib as L
-import ctn_ops as ops
-from conv_tasnet import ConvTasNet, _act_dtype, _mask_code, _norm_code
+from conv_tasnet import ConvTasNet, _mask_code, _norm_code
+
+
+def _t1x1(conv: nn.Conv1d) -> torch.Tensor:
+    """Conv1d(cin, cout, 1).weight [cout, cin, 1] -> [cin, cout] fp32 contiguous."""
+    return conv.weight.detach()[:, :, 0].t().contiguous().float()
+
+
+def _norm_pair(norm: nn.Module):
+    """cLN -> (gamma, beta); eval BatchNorm1d -> (scale, shift) with its running stats."""
+    if isinstance(norm, nn.BatchNorm1d):
+        scale = norm.weight.detach() / torch.sqrt(norm.running_var.detach() + norm.eps)
+        return scale.float().contiguous(), (norm.bias.detach() - norm.running_mean.detach() * scale).float().contiguous()
+    return norm.gamma.detach().reshape(-1).float().contiguous(), norm.beta.detach().reshape(-1).float().contiguous()
 
 
 class StreamingSeparator:
@@ -43,7 +57,7 @@ class StreamingSeparator:
     >>> outs.append(s.flush())                  # the last L/2 samples
     """
 
-    def __init__(self, model: ConvTasNet, act_dtype=None):
+    def __init__(self, model: ConvTasNet, act_dtype=None, max_frames: int = 64):
         if not model.causal:
             raise ValueError("streaming needs a causal model (ConvTasNet(causal=True))")
         norm = _norm_code(model.norm_type)
@@ -53,38 +67,90 @@ class StreamingSeparator:
             raise ValueError("BatchNorm streams only in eval mode (running statistics)")
         if model.L % 2:
             raise ValueError("the encoder stride L//2 must tile the frame (even L)")
+        if act_dtype not in (None, torch.float32):
+            raise ValueError("streaming computes in fp32")
         self.model = model
         self.norm = norm
-        self.dt = _act_dtype(act_dtype if act_dtype is not None else model.act_dtype)
         self.stride = model.L // 2
-        self.blocks = list(model.separator.blocks())
-        # frames of history per block: (P-1)*dilation (the causal receptive field)
-        self.ctx = [(b._geo[2] - 1) * b._geo[3] for b in self.blocks]
+        self.max_frames = int(max_frames)
+        self.lib = L.load()
+        self.refresh_weights()
         self.reset()
+
+    def refresh_weights(self):
+        """Snapshot the model's parameters in the layouts the stream kernels read."""
+        m = self.model
+        sep = m.separator
+        cln, bott, _, mask = sep.network
+        self.U = m.encoder.conv1d_U.weight.detach()[:, 0, :].float().contiguous()          # [N][L]
+        self.g0, self.b0 = _norm_pair(cln)
+        self.wb_t = _t1x1(bott)                                                             # [N][B]
+        self.wm_t = _t1x1(mask)                                                             # [B][C*N]
+        self.V = m.decoder.basis_signals.weight.detach().float().contiguous()              # [L][N]
+        self.blocks = []
+        for blk in sep.blocks():
+            B, H, P, dil, _, _ = blk._geo
+            ds = blk.net[3].net
+            n1, n2 = blk._norms()
+            a1, b1 = _norm_pair(n1)
+            a2, b2 = _norm_pair(n2)
+            self.blocks.append(dict(
+                dil=dil, P=P, w1_t=_t1x1(blk.net[0]), alpha1=blk.net[1].weight.detach().float().contiguous(),
+                n1a=a1, n1b=b1, wd=ds[0].weight.detach()[:, 0, :].float().contiguous(),
+                alpha2=ds[2].weight.detach().float().contiguous(), n2a=a2, n2b=b2, w2_t=_t1x1(ds[4])))
+        self.B, self.H = self.blocks[0]["w1_t"].shape if self.blocks else (bott.weight.shape[0], 0)
 
     def reset(self):
         self.samples = None          # [M, s] pending input samples
-        self.hist = [None] * len(self.blocks)   # [M, h, B] block-input history
+        self.rings = None            # per block [M, R, H]
         self.tail = None             # [M, C, stride] pending overlap-add samples
-        self.frames = 0              # frames emitted so far
+        self.frames = 0              # frames emitted so far (= pos of the next frame)
 
     @property
     def latency_samples(self) -> int:
         """Output trails input by one stride: the last L/2 samples wait for the next frame."""
         return self.stride
 
-    # -- helpers ---------------------------------------------------------------
-    def _pad_rows(self, seq: torch.Tensor) -> tuple:
-        """[M, K, C] frames -> ([M*Kp, C] rows with zero padded rows, Frames)."""
-        M, K, C = seq.shape
-        fr = ops.Frames.of(M, K)
-        rows = seq.new_zeros(M, fr.Kp, C)
-        rows[:, :K] = seq
-        return rows.view(M * fr.Kp, C), fr
+    def _desc(self, M, K):
+        m = self.model
+        return L.StreamDesc(M, K, m.N, m.L, self.B, self.H, m.P, m.C,
+                            L.NORM_CLN if self.norm == L.NORM_CLN else L.NORM_BN, _mask_code(m.mask_nonlinear))
 
-    @staticmethod
-    def _frames(rows: torch.Tensor, fr: ops.Frames, first: int = 0) -> torch.Tensor:
-        return rows.view(fr.M, fr.Kp, -1)[:, first:fr.K]
+    def _alloc(self, M, dev):
+        self.rings = []
+        for b in self.blocks:
+            need = (b["P"] - 1) * b["dil"] + self.max_frames
+            R = 1 << max(0, (need - 1).bit_length())
+            self.rings.append(torch.zeros(M, R, self.H, device=dev))
+        self.tail = torch.zeros(M, self.model.C, self.stride, device=dev)
+
+    def _call(self, buf: torch.Tensor, K: int) -> torch.Tensor:
+        """K frames whose samples start at buf[:, 0] -> [M, C, K*stride] finished samples."""
+        m, lib = self.model, self.lib
+        M, dev = buf.shape[0], buf.device
+        d = self._desc(M, K)
+        st = L.stream_handle(dev)
+        w = torch.empty(M, K, m.N, device=dev)
+        x = torch.empty(M, K, self.B, device=dev)
+        L.check(lib.ctn_stream_encode(ctypes.byref(d), buf.data_ptr(), buf.stride(0), self.U.data_ptr(),
+                                      self.g0.data_ptr(), self.b0.data_ptr(), self.wb_t.data_ptr(), w.data_ptr(),
+                                      x.data_ptr(), st), "ctn_stream_encode")
+        y = torch.empty_like(x)
+        for b, ring in zip(self.blocks, self.rings):
+            L.check(lib.ctn_stream_block(ctypes.byref(d), b["dil"], self.frames, ring.shape[1], x.data_ptr(),
+                                         *(b[k].data_ptr() for k in ("w1_t", "alpha1", "n1a", "n1b", "wd", "alpha2",
+                                                                     "n2a", "n2b", "w2_t")),
+                                         ring.data_ptr(), y.data_ptr(), st), "ctn_stream_block")
+            x, y = y, x
+        out = torch.empty(M, m.C, K * self.stride, device=dev)
+        frames = torch.empty(M, m.C, K, m.L, device=dev)
+        tail = torch.empty_like(self.tail)
+        L.check(lib.ctn_stream_decode(ctypes.byref(d), x.data_ptr(), w.data_ptr(), self.wm_t.data_ptr(),
+                                      self.V.data_ptr(), self.tail.data_ptr(), tail.data_ptr(), frames.data_ptr(),
+                                      out.data_ptr(), st), "ctn_stream_decode")
+        self.tail = tail
+        self.frames += K
+        return out
 
     # -- streaming -------------------------------------------------------------
     @torch.no_grad()
@@ -95,43 +161,25 @@ class StreamingSeparator:
         chunk = chunk.float()
         buf = chunk if self.samples is None else torch.cat([self.samples, chunk], dim=1)
         M, T = buf.shape
+        if self.rings is None:
+            self._alloc(M, buf.device)
+        elif self.tail.shape[0] != M:
+            raise ValueError("the number of streams changed; call reset() first")
         K = (T - m.L) // self.stride + 1 if T >= m.L else 0
         if K <= 0:
             self.samples = buf
             return buf.new_zeros(M, m.C, 0)
-        used = (K - 1) * self.stride + m.L
-        self.samples = buf[:, K * self.stride:]        # the overlap of the next frame onwards
-        enc_in = buf[:, :used].contiguous()
-
-        sep = m.separator
-        cln, bott = sep.network[0], sep.network[1]
-        fr = ops.Frames.of(M, K)
-        w_rows, x = ops.EncoderFn.apply(enc_in, fr, (m.N, m.L, m.B, m.C), self.dt, m.encoder.conv1d_U.weight,
-                                        cln.gamma, cln.beta, bott.weight)
-        new = self._frames(x, fr)                       # [M, K, B]
-        for i, blk in enumerate(self.blocks):
-            h = self.hist[i]
-            seq = new if h is None else torch.cat([h, new], dim=1)
-            rows, fr_b = self._pad_rows(seq)
-            y = blk._forward_rows(rows, fr_b, self.norm)
-            hn = seq.shape[1] - K                       # history frames in front of the new ones
-            keep = self.ctx[i]
-            self.hist[i] = seq[:, max(0, seq.shape[1] - keep):].clone() if keep > 0 else None
-            new = self._frames(y, fr_b, hn)
-        x_last, _ = self._pad_rows(new)
-        Tc = (K - 1) * self.stride + m.L
-        est = ops.DecoderFn.apply(x_last, w_rows, fr, (Tc, m.N, m.L, m.B, m.C, _mask_code(m.mask_nonlinear)),
-                                  sep.network[3].weight, m.decoder.basis_signals.weight)   # [M, C, Tc]
-        if self.tail is not None:
-            est[:, :, :self.stride] += self.tail
-        self.tail = est[:, :, K * self.stride:].clone()
-        self.frames += K
-        return est[:, :, :K * self.stride]
+        outs = []
+        for k0 in range(0, K, self.max_frames):
+            k = min(self.max_frames, K - k0)
+            outs.append(self._call(buf[:, k0 * self.stride:].contiguous(), k))
+        self.samples = buf[:, K * self.stride:].contiguous()    # the overlap of the next frame onwards
+        return outs[0] if len(outs) == 1 else torch.cat(outs, dim=2)
 
     @torch.no_grad()
     def flush(self) -> torch.Tensor:
         """The remaining overlap-add samples (call once after the last chunk)."""
-        out = self.tail
+        out = self.tail if self.frames else None
         self.tail = None
         if out is None:
             return torch.zeros(0)

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define CTN_ABI_VERSION 4
+#define CTN_ABI_VERSION 5
 
 typedef enum { CTN_DTYPE_F32 = 0, CTN_DTYPE_BF16 = 1 } ctn_dtype;
 /* CTN_NORM_BN: torch.nn.BatchNorm1d, chose_norm's fallback branch (conv_tasnet.py:302-303) */
@@ -261,6 +261,43 @@ int ctn_conv1x1_backward(const ctn_rows_desc* d, int cout, const void* x, const 
 int ctn_mask_forward(const ctn_rows_desc* d, int nspk, int mask_type, const void* score, void* mask, void* stream);
 int ctn_mask_backward(const ctn_rows_desc* d, int nspk, int mask_type, const void* score, const void* gmask,
                       void* gscore, void* stream);
+
+/* -------------------------------------------------------------------------
+ * Streaming causal separation: replaces running src/separate.py:35-79 on a
+ * causal model (conv_tasnet.py:176 Chomp1d, :289) whole-signal, with chunked
+ * calls that carry state instead of re-running history.  fp32.
+ * Frame k of a stream covers samples [k*L/2, k*L/2 + L).  State per
+ * TemporalBlock: `ring` [M][ring_frames][H], the block's depthwise-conv input
+ * frames (after conv1x1, PReLU and norm 1), frame g at slot g % ring_frames;
+ * ring_frames a power of two >= (P-1)*dilation + K.  `pos` = frames of this
+ * stream processed before the call (taps before frame 0 read as zero: the
+ * reference's causal zero padding).  1x1 weights are passed TRANSPOSED,
+ * [in][out]: wb_t [N][B], w1_t [B][H], w2_t [H][B], wm_t [B][C*N]; wd [H][P];
+ * U [N][L]; V [L][N] (Linear(N, L).weight).  norm CTN_NORM_CLN takes
+ * gamma/beta, CTN_NORM_BN an eval-mode BatchNorm folded to scale/shift.
+ * encode: samples [M][ld] (the call's (K-1)*L/2 + L samples at offset 0)
+ *         -> w_out [M][K][N] (ReLU(U*frame)), x_out [M][K][B] (cLN, bottleneck)
+ * block : x_in [M][K][B] -> ring (new frames), x_out [M][K][B]
+ * decode: x_last, w -> out [M][C][K*L/2]: the K frames overlap-added with
+ *         tail_in [M][C][L/2] (zeros at the stream start); tail_out gets the
+ *         last frame's second half.  frames_ws: [M][C][K][L] scratch.
+ * ------------------------------------------------------------------------- */
+typedef struct {
+  int32_t M, K;
+  int32_t N, L, B, H, P, C;
+  int32_t norm;      /* CTN_NORM_CLN or CTN_NORM_BN (eval, affine) */
+  int32_t mask_type; /* ctn_mask_type or CTN_MASK_IDENTITY */
+} ctn_stream_desc;
+int ctn_stream_encode(const ctn_stream_desc* d, const float* samples, int64_t ld_samples, const float* U,
+                      const float* gamma0, const float* beta0, const float* wb_t, float* w_out, float* x_out,
+                      void* stream);
+int ctn_stream_block(const ctn_stream_desc* d, int dilation, int64_t pos, int ring_frames, const float* x_in,
+                     const float* w1_t, const float* alpha1, const float* norm1_a, const float* norm1_b,
+                     const float* wd, const float* alpha2, const float* norm2_a, const float* norm2_b,
+                     const float* w2_t, float* ring, float* x_out, void* stream);
+int ctn_stream_decode(const ctn_stream_desc* d, const float* x_last, const float* w, const float* wm_t,
+                      const float* V, const float* tail_in, float* tail_out, float* frames_ws, float* out,
+                      void* stream);
 
 /* -------------------------------------------------------------------------
  * Opt-in kernel timer (bench.py roofline): when enabled, every launch of the

@@ -170,9 +170,13 @@ def _hip_model(cfg_d, params, act_dtype):
 def test_model_bench_step_bf16_vs_oracle():
     """The bench's c2 step exactly: paper config, 32 utterances of 4 s @ 8 kHz from
     synthetic.speech_like(seed 1234) — the bench's inputs — bf16 activations, packed
-    weights.  Every utterance's SI-SNR and the loss within 0.1 dB of the fp32 oracle;
-    first/middle/last estimates within 5e-2; weight gradients within 0.1 relative
-    L2 of the full-batch oracle gradients (bf16 activations through 32 blocks)."""
+    weights, RANDOM weights.  Loss within 0.05 dB of the fp32 oracle; per-utterance
+    SI-SNR median within 0.05 dB and every utterance within 0.25 dB (random weights put
+    every estimate near -22 dB SI-SNR, where bf16's ~3e-3 relative error of the estimate
+    moves the small target projection by up to ~0.2 dB); first/middle/last estimates
+    within 5e-2; weight gradients within 0.1 relative L2 of the full-batch oracle
+    gradients (bf16 activations through 32 blocks).  The north-star 0.1 dB bar on a
+    SEPARATING paper-config model at this same shape is test_gpu_paper_trained.py."""
     import pit_criterion as pc
     import synthetic
     torch.manual_seed(0)
@@ -190,9 +194,6 @@ def test_model_bench_step_bf16_vs_oracle():
     snr = max_snr.detach().cpu().reshape(-1)
     dsnr = (snr - snr_r).abs()
     print("loss", float(loss), loss_r, "SI-SNR diff per utt: median", float(dsnr.median()), "max", float(dsnr.max()))
-    # random weights put every estimate near -22 dB SI-SNR, where the small target
-    # projection amplifies bf16's ~3e-3 relative error of the estimate into ~0.1 dB;
-    # the north-star 0.1 dB SI-SNRi bar on a SEPARATING model is test_trained_model_sisnri
     assert abs(float(loss) - loss_r) < 0.05
     assert float(dsnr.median()) < 0.05 and float(dsnr.max()) < 0.25, dsnr
     for b in (0, M // 2, M - 1):
@@ -331,3 +332,40 @@ def test_train_step_c1_fp32_vs_reference_step():
         total += d.size
         assert d.max() <= 2.1e-3, (n, d.max())   # at most one full sign flip of a ~0 gradient
     assert off <= max(2, total // 2000), (off, total)
+
+
+@pytest.mark.timeout(900)
+def test_model_c4_shape_bf16_vs_oracle():
+    """c4's per-GPU dispatch exactly (BASELINE.json configs[3]): causal cLN, L=16, 16 kHz,
+    64 utterances of 4 s (K=7999 frames, Kp=8064) in one bf16 forward + PIT loss +
+    backward, random weights.  cLN and the causal depthwise convolution act per frame /
+    per utterance, so the first, middle and last utterances are checked against the fp32
+    oracle run on those three alone: estimates within 5e-2 relative L2; per-utterance
+    SI-SNR within 1 dB only, because random causal-cLN weights put every estimate near
+    -33 dB SI-SNR, where the target projection is ~2 % of the estimate's norm and bf16's
+    ~3e-3 relative error of the estimate moves it by tenths of a dB (measured 0.27 dB);
+    every weight gradient finite."""
+    import pit_criterion as pc
+    import synthetic
+    cfg_d = dict(PAPER, L=16, norm_type="cLN", causal=True)
+    cfg = O.Cfg(**cfg_d)
+    params = O.init_params(cfg, 4)
+    M, T = 64, 64000
+    mix, src = synthetic.speech_like(M, 2, T, 4321)
+    lens = torch.full((M,), T, dtype=torch.int64)
+    model = _hip_model(cfg_d, params, torch.bfloat16)
+    est = model(mix.to(DEV))
+    loss, max_snr, est_m, _ = pc.cal_loss(src.to(DEV), est, lens.to(DEV))
+    model.zero_grad()
+    loss.backward()
+    snr = max_snr.detach().cpu().reshape(-1)
+    for b in (0, M // 2, M - 1):
+        with torch.no_grad():
+            e_r = O.model_forward(cfg, mix[b:b + 1], params)
+            ms_r = O.si_snr_pit(src[b:b + 1], e_r, lens[b:b + 1])[0]
+        r = rel(est_m[b].detach().cpu(), e_r[0])
+        print("c4 utterance", b, "est rel L2", r, "SI-SNR", float(snr[b]), float(ms_r.reshape(-1)[0]))
+        assert r < 5e-2, b
+        assert abs(float(snr[b]) - float(ms_r.reshape(-1)[0])) < 1.0, (b, float(snr[b]), float(ms_r))
+    for n, p in model.named_parameters():
+        assert torch.isfinite(p.grad).all(), n

@@ -1,0 +1,48 @@
+"""Separating paper-config parity at the north-star tolerance (BASELINE.json): the
+bench workload's shape (32 utterances x 4 s @ 8 kHz, paper config N=256 L=20 B=256
+H=512 P=3 X=8 R=4 gLN) through the HIP path with weights trained until the model
+separates (tests/golden/make_golden_paper_trained.py; reference SI-SNRi per utterance
+from jwr1995/Conv-TasNet's own cal_SISNRi).  bf16 activations: every utterance's
+SI-SNRi within 0.1 dB of the reference's; fp32 mode within 0.01 dB."""
+import numpy as np
+import pytest
+import torch
+
+import paper_fixture as PF
+from oracle import ctn_oracle as O
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not PF.available(), reason="model_paper_trained.npz not generated")]
+
+
+def _sisnri(dtype):
+    import conv_tasnet as ct
+    import pit_criterion as pc
+    params, mix, src, g = PF.load()
+    c = PF.CFG
+    model = ct.ConvTasNet(c.N, c.L, c.B, c.H, c.P, c.X, c.R, c.C).cuda()
+    model.load_state_dict(params)
+    model.act_dtype = dtype
+    lens = torch.full((mix.shape[0],), mix.shape[1], dtype=torch.int64, device="cuda")
+    with torch.no_grad():
+        est = model(mix.cuda())
+        loss, max_snr, est_m, reord = pc.cal_loss(src.cuda(), est, lens)
+    reord = reord.cpu().numpy()
+    got = np.array([O.cal_sisnri(src[b].numpy(), reord[b], mix[b].numpy()) for b in range(mix.shape[0])])
+    return got, g, float(loss)
+
+
+def test_paper_trained_bf16_sisnri_within_0p1db():
+    got, g, loss = _sisnri(torch.bfloat16)
+    ref = g["sisnri"]
+    assert ref.mean() > 3.0, "fixture model should separate"
+    d = np.abs(got - ref)
+    assert d.max() < 0.1, (d.max(), int(d.argmax()), got[d.argmax()], ref[d.argmax()])
+    assert abs(loss - float(g["loss"])) < 0.1
+
+
+def test_paper_trained_fp32_sisnri_within_0p01db():
+    got, g, loss = _sisnri(torch.float32)
+    d = np.abs(got - g["sisnri"])
+    assert d.max() < 0.01, d.max()
+    assert abs(loss - float(g["loss"])) < 1e-3

@@ -196,3 +196,18 @@ def test_trained_model_fixture():
         l = int(g["len"][b])
         v = O.cal_sisnri(g["src"][b, :, :l], reord[b, :, :l].numpy(), g["mix"][b, :l])
         assert abs(v - g["sisnri"][b]) < 1e-3
+
+
+def test_paper_trained_fixture_oracle():
+    """The oracle on the separating paper-config fixture (two of its utterances, to keep
+    the CPU suite short): per-utterance SI-SNRi equal to the reference's."""
+    import paper_fixture as PF
+    if not PF.available():
+        pytest.skip("model_paper_trained.npz not generated")
+    params, mix, src, g = PF.load()
+    for b in (0, 17):
+        est = O.model_forward(PF.CFG, mix[b:b + 1], params)
+        lens = torch.tensor([mix.shape[1]])
+        _, _, _, reord = O.cal_loss(src[b:b + 1], est, lens)
+        v = O.cal_sisnri(src[b].numpy(), reord[0].detach().numpy(), mix[b].numpy())
+        assert abs(v - g["sisnri"][b]) < 1e-3, (b, v, g["sisnri"][b])
