@@ -385,9 +385,20 @@ struct StatFold {
 CTN_DEV float2 fold_stat(const StatFold& f, int m) {
   double s = 0.0, ss = 0.0;
   const int lane = (int)(threadIdx.x & 63);
+  // Each lane sums its partials i = lane, lane+64, ... in that order; the loads of four
+  // consecutive ones are issued together (a load-add chain would pay one memory latency
+  // per partial, serially, at the start of every consumer workgroup).
   if (f.ws.grid == 0) {
     const double2* sg = f.slab + (size_t)m * f.parts;
-    for (int i = lane; i < f.parts; i += 64) {
+    int i = lane;
+    for (; i + 192 < f.parts; i += 256) {
+      const double2 v0 = sg[i], v1 = sg[i + 64], v2 = sg[i + 128], v3 = sg[i + 192];
+      s += v0.x; ss += v0.y;
+      s += v1.x; ss += v1.y;
+      s += v2.x; ss += v2.y;
+      s += v3.x; ss += v3.y;
+    }
+    for (; i < f.parts; i += 64) {
       const double2 v = sg[i];
       s += v.x;
       ss += v.y;
@@ -396,14 +407,24 @@ CTN_DEV float2 fold_stat(const StatFold& f, int m) {
     const WsRuns& w = f.ws;
     const int blo = ws_block_of_tile(w, m * w.tpu), bhi = ws_block_of_tile(w, (m + 1) * w.tpu - 1);
     const int n = (bhi - blo + 1) * w.waves;
-    for (int i = lane; i < n; i += 64) {
+    auto get = [&](int i) {   // partial i of utterance m, or zero for a range that stored none
       const int b = blo + i / w.waves, wv = i % w.waves;
       const int t0 = ws_t0(w, b);
-      if (t0 < ws_t0(w, b + 1)) {   // empty ranges stored nothing
-        const double2 v = f.slab[((size_t)b * w.waves + wv) * w.kmax + (m - t0 / w.tpu)];
-        s += v.x;
-        ss += v.y;
-      }
+      return t0 < ws_t0(w, b + 1) ? f.slab[((size_t)b * w.waves + wv) * w.kmax + (m - t0 / w.tpu)]
+                                  : make_double2(0.0, 0.0);
+    };
+    int i = lane;
+    for (; i + 192 < n; i += 256) {
+      const double2 v0 = get(i), v1 = get(i + 64), v2 = get(i + 128), v3 = get(i + 192);
+      s += v0.x; ss += v0.y;
+      s += v1.x; ss += v1.y;
+      s += v2.x; ss += v2.y;
+      s += v3.x; ss += v3.y;
+    }
+    for (; i < n; i += 64) {
+      const double2 v = get(i);
+      s += v.x;
+      ss += v.y;
     }
   }
   s = wave_sum(s);

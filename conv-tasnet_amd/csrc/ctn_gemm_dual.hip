@@ -71,6 +71,10 @@ constexpr int DU_MMAX = 512;   // utterances whose gLN statistics a workgroup ho
 #ifndef CTN_DU_DBG
 #define CTN_DU_DBG 0
 #endif
+// experiment: 1 raises the wave priority (s_setprio 1) while it issues a tile's MFMAs
+#ifndef CTN_DU_PRIO
+#define CTN_DU_PRIO 0
+#endif
 #ifndef CTN_DU_LATE
 #define CTN_DU_LATE 0
 #endif
@@ -376,6 +380,7 @@ __global__ __launch_bounds__(DU_NT) void gemm_dual_kernel(GemmDual p) {
   };
 
   auto compute = [&](int t, f32x4_t (&acc)[NBW]) __attribute__((always_inline)) {
+    if constexpr (CTN_DU_PRIO) __builtin_amdgcn_s_setprio(1);
     const char* a = smem + OFF_A + (t % D) * A_SZ;
     const char* bsl = BXF ? smem + OFF_BI + (t & 1) * B_SZ : smem + OFF_B + (t % D) * B_SZ;
 #pragma unroll
@@ -407,6 +412,7 @@ __global__ __launch_bounds__(DU_NT) void gemm_dual_kernel(GemmDual p) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         dacc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], dacc[i][j], 0, 0, 0);
+    if constexpr (CTN_DU_PRIO) __builtin_amdgcn_s_setprio(0);
   };
 
   // row epilogue of tile t: lane holds row t*TM + erow, channels colbase..+NV -> C image (t & 1)

@@ -48,7 +48,8 @@ constexpr int WS_DR = CTN_WS_DR;
 constexpr int WS_FOLD_MAX = 512;   // utterances whose gLN operand stats a workgroup holds in LDS
 
 // Bound-finding experiments only (tools/microbench): bit 0 drops the output
-// stores, bit 1 the A-tile loads, bit 2 the MFMAs, bit 3 the epilogue math.
+// stores, bit 1 the A-tile loads, bit 2 the MFMAs, bit 3 the epilogue math; bit 6
+// (experiment, not bound-finding) lets the scheduler move epilogue math into the MFMAs.
 #ifndef CTN_WS_EXP
 #define CTN_WS_EXP 0
 #endif
@@ -78,6 +79,10 @@ constexpr int WS_FOLD_MAX = 512;   // utterances whose gLN operand stats a workg
 #endif
 #ifndef CTN_WS_LA8
 #define CTN_WS_LA8 3
+#endif
+// experiment: 1 raises the wave priority (s_setprio 1) while it issues a tile's MFMAs
+#ifndef CTN_WS_PRIO
+#define CTN_WS_PRIO 0
 #endif
 #ifndef CTN_WS_STAMP
 #define CTN_WS_STAMP 0
@@ -171,11 +176,14 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
   if constexpr (FOLDS) {
     const StatFold& f = p.aop.fold;
     if (f.slab) {
-      for (int gi = wid; gi < p.g.M; gi += WV) {
+      // only the utterances of this workgroup's rows (one per wave, in parallel); the
+      // workgroup holding an utterance's first row stores its pair for backward
+      const int mlo = (int)((long)t0 * TM / Kp), mhi = t1 > t0 ? (int)(((long)t1 * TM - 1) / Kp) : mlo - 1;
+      for (int gi = mlo + wid; gi <= mhi; gi += WV) {
         const float2 v = fold_stat(f, gi);
         if (lane == 0) {
           sst[gi] = v;
-          if (f.out && blockIdx.x == 0) f.out[gi] = v;   // saved for backward
+          if (f.out && (long)gi * Kp >= (long)t0 * TM) f.out[gi] = v;   // saved for backward
         }
       }
     } else {
@@ -324,6 +332,7 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
   // just before them (one read in flight per step exposed the LDS latency 16x/tile).
   constexpr int LA = SWP ? 0 : WV == 16 ? CTN_WS_LA16 : CTN_WS_LA8;
   auto mfma_tile = [&](const char* buf, f32x4_t (&acc)[MB][NB]) __attribute__((always_inline)) {
+    if constexpr (CTN_WS_PRIO) __builtin_amdgcn_s_setprio(1);   // experiment: MFMA issue first
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
@@ -359,6 +368,7 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
         __builtin_amdgcn_sched_group_barrier(0x008, MB * NB, 0);
       }
     }
+    if constexpr (CTN_WS_PRIO) __builtin_amdgcn_s_setprio(0);
   };
 
   // gLN run partial of this wave (WsRuns layout); every lane stores the same value
@@ -573,7 +583,7 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
         if (t > t0) cln_final(t - 1);
         dma(t + WS_DR - 1);
         mfma_tile(sA[t % WS_DR], acc);
-        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (!(CTN_WS_EXP & 64)) __builtin_amdgcn_sched_barrier(0);
         epilogue_math(le1, t, acc);
         store_out(t);
       }
@@ -595,7 +605,7 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
             if (t > t0) cln_final(t - 1);
             WS_STAMP(0);
             mfma_tile(sA[t & 1], acc);
-            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (!(CTN_WS_EXP & 64)) __builtin_amdgcn_sched_barrier(0);
             WS_STAMP(1);
             if constexpr (CTN_WS_ORDER == 1) {
               // next tile's operand (its buffer's last reader finished before the barrier)
