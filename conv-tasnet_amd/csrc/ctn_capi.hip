@@ -564,9 +564,12 @@ extern "C" int ctn_tblock_forward(const ctn_tblock_desc* d, const ctn_tblock_par
 
   const void* w1 = p->w1;
   const void* w2 = p->w2;
+  const void *w1f = nullptr, *w2f = nullptr;   // fragment-ordered copies (caller packs only)
   if (dt == BF16 && p->w1_bf16 && p->w2_bf16) {   // packed once per step by the caller
     w1 = p->w1_bf16;
     w2 = p->w2_bf16;
+    w1f = p->w1_frag;
+    w2f = p->w2_frag;
   } else if (dt == BF16) {
     PrepBatch pb{};
     pb.d[0] = PrepDesc{p->w1, d->H, d->B, L.w1s, nullptr};
@@ -580,6 +583,7 @@ extern "C" int ctn_tblock_forward(const ctn_tblock_desc* d, const ctn_tblock_par
   GemmRows g1 = tb_gemm1(d);
   g1.A = x;
   g1.W = w1;
+  g1.Wf = w1f;
   g1.alpha = p->alpha1;
   g1.C = sv->h1;
   g1.grp_slab = L.slab1;
@@ -619,7 +623,7 @@ extern "C" int ctn_tblock_forward(const ctn_tblock_desc* d, const ctn_tblock_par
   g2.A = sv->d; g2.lda = d->H;
   g2.aop.kind = OP_PRELU_NORM; g2.aop.norm = d->norm_type; g2.aop.stats = st2;
   g2.aop.gamma = p->gamma2; g2.aop.beta = p->beta2; g2.aop.alpha = p->alpha2;
-  g2.W = w2; g2.ldw = d->H;
+  g2.W = w2; g2.ldw = d->H; g2.Wf = w2f;
   g2.epi = EPI_RESID; g2.R = x; g2.ldr = d->B;
   g2.C = y; g2.ldc = d->B;
   if (fold && gemm_ws_can_fold(dt, g2)) g2.aop.fold = StatFold{L.slab2, L.parts2, cnt, (float)kEps, 0, st2};
@@ -647,9 +651,12 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
 
   const void* w1t = L.w1t;
   const void* w2t = L.w2t;
+  const void *w1tf = nullptr, *w2tf = nullptr;   // fragment-ordered copies (caller packs only)
   if (dt == BF16 && p->w1t_bf16 && p->w2t_bf16) {   // packed once per step by the caller
     w1t = p->w1t_bf16;
     w2t = p->w2t_bf16;
+    w1tf = p->w1t_frag;
+    w2tf = p->w2t_frag;
   } else {
     PrepBatch pb{};
     pb.d[0] = PrepDesc{p->w2, d->B, d->H, nullptr, L.w2t};   // [H][B]
@@ -663,12 +670,13 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
   GemmRows ga = tb_gemmA(d);
   ga.A = gy;
   ga.W = w2t;
+  ga.Wf = w2tf;
   ga.R = sv->d;
   ga.alpha = p->alpha2; ga.stats = st2; ga.gamma = p->gamma2;
   ga.C = L.G1;
   ga.grp_slab = L.slabA;
   GemmDual duA = tb_dualA(d);
-  duA.A = gy; duA.W = w2t; duA.R = sv->d; duA.C = L.G1;
+  duA.A = gy; duA.W = w2t; duA.Wf = w2tf; duA.R = sv->d; duA.C = L.G1;
   duA.alpha = p->alpha2; duA.stats = st2; duA.gamma = p->gamma2; duA.grp_slab = L.slabA;
   duA.Bm = sv->d;
   duA.bop.stats = st2; duA.bop.gamma = p->gamma2; duA.bop.beta = p->beta2; duA.bop.alpha = p->alpha2;
@@ -716,7 +724,7 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
     //       gradient and stores gh1 = dL/dh1 to G1 on the way (one pass instead of
     //       norm1_bwd's write + the GEMM's re-read)
     GemmRows gb = tb_gemmB(d, true);
-    gb.A = L.G2; gb.W = w1t; gb.R = gy; gb.C = gx;
+    gb.A = L.G2; gb.W = w1t; gb.Wf = w1tf; gb.R = gy; gb.C = gx;
     gb.aop.stats = st1; gb.aop.alpha = p->alpha1; gb.aop.aux = sv->h1; gb.aop.apart = L.alphaSlab;
     gb.aop.aout = L.G1;
     if (fold) gb.aop.fold = StatFold{L.slabD, L.partsD, cnt, 0.f, 1, nullptr};
@@ -740,7 +748,7 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
     // (e) gx = gh1 . W1 + gy
     // (f) dW1 = gh1^T . x                          — one dual-GEMM pass when eligible
     GemmDual duB = tb_dualB(d);
-    duB.A = L.G1; duB.W = w1t; duB.R = gy; duB.C = gx;
+    duB.A = L.G1; duB.W = w1t; duB.Wf = w1tf; duB.R = gy; duB.C = gx;
     duB.Bm = x; duB.Dpart = L.cpart1;
     if (gemm_dual_eligible(dt, duB)) {
       CTN_HIP(launch_gemm_dual(duB, s));
@@ -748,7 +756,7 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
       GemmRows gb{};
       gb.g = rg; gb.Kred = d->H; gb.Nout = d->B; gb.norm = d->norm_type;
       gb.A = L.G1; gb.lda = d->H;
-      gb.W = w1t; gb.ldw = d->H;
+      gb.W = w1t; gb.ldw = d->H; gb.Wf = w1tf;
       gb.epi = EPI_RESID; gb.R = gy; gb.ldr = d->B;
       gb.C = gx; gb.ldc = d->B;
       CTN_HIP(launch_gemm_rows(dt, gb, s));
@@ -1243,15 +1251,20 @@ static_assert(sizeof(ctn_weight_pack) == sizeof(PrepDesc), "pack layout");
 
 extern "C" int ctn_pack_weights(const ctn_weight_pack* packs, int n, void* stream) {
   if (n < 0 || (n > 0 && !packs)) return fail(CTN_ERR_ARG, "ctn_pack_weights: bad table");
-  for (int i = 0; i < n; ++i)
-    if (!packs[i].src || packs[i].rows <= 0 || packs[i].cols <= 0 || (!packs[i].dst && !packs[i].dst_t))
+  for (int i = 0; i < n; ++i) {
+    const ctn_weight_pack& w = packs[i];
+    if (!w.src || w.rows <= 0 || w.cols <= 0 || (!w.dst && !w.dst_t && !w.dst_frag && !w.dst_t_frag))
       return fail(CTN_ERR_ARG, "ctn_pack_weights: entry %d is empty or has no destination", i);
+    if ((w.dst_frag || w.dst_t_frag) && (w.rows % 32 || w.cols % 32))
+      return fail(CTN_ERR_ARG, "ctn_pack_weights: entry %d: fragment order needs rows and cols in multiples of 32 "
+                  "(%d x %d)", i, w.rows, w.cols);
+  }
   for (int i0 = 0; i0 < n; i0 += PREP_MAX) {
     PrepBatch pb{};
     pb.nd = n - i0 < PREP_MAX ? n - i0 : PREP_MAX;
     for (int i = 0; i < pb.nd; ++i) {
       const ctn_weight_pack& w = packs[i0 + i];
-      pb.d[i] = PrepDesc{w.src, w.rows, w.cols, w.dst, w.dst_t};
+      pb.d[i] = PrepDesc{w.src, w.rows, w.cols, w.dst, w.dst_t, w.dst_frag, w.dst_t_frag};
     }
     CTN_HIP(launch_prep_weights(BF16, pb, (hipStream_t)stream));
   }

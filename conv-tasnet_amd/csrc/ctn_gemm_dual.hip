@@ -75,6 +75,13 @@ constexpr int DU_MMAX = 512;   // utterances whose gLN statistics a workgroup ho
 #ifndef CTN_DU_PRIO
 #define CTN_DU_PRIO 0
 #endif
+// 1: the resident weight and constants are loaded and waited for before the first DMA
+// groups are issued (round-2 order); 0 (experiment): the first D-1 DMA groups go out
+// first, so their latency overlaps the weight's.  0 makes the cLN epilogue statistics
+// of the first tiles irreproducible in every launch and gains nothing.
+#ifndef CTN_DU_EARLY
+#define CTN_DU_EARLY 1
+#endif
 #ifndef CTN_DU_LATE
 #define CTN_DU_LATE 0
 #endif
@@ -218,30 +225,6 @@ __global__ __launch_bounds__(DU_NT) void gemm_dual_kernel(GemmDual p) {
   //      NV contiguous output channels)
   const int mbw = wid / WNB, nbg = wid % WNB;
   const int colbase = n0 + nbg * 16 * NBW + lg * NV;
-  v4u wf[NBW][KB];
-#pragma unroll
-  for (int nb = 0; nb < NBW; ++nb) {
-    const int n = n0 + nbg * 16 * NBW + (lr >> 2) * NV + nb * 4 + (lr & 3);
-#pragma unroll
-    for (int kb = 0; kb < KB; ++kb) wf[nb][kb] = ldg16(W + (size_t)n * p.ldw + kb * 32 + lg * 8);
-  }
-  const float eal = EPI == EPI_NORM_BWD ? p.alpha[0] : 0.f;
-  const float bal = OPB == OP_PRELU_NORM ? p.bop.alpha[0] : 0.f;
-  for (int c = tid; c < NS; c += NT) {
-    sg[c] = BXF ? p.bop.gamma[n0 + c] : 0.f;
-    sg[NS + c] = BXF ? p.bop.beta[n0 + c] : 0.f;
-    sg[2 * NS + c] = EPI == EPI_NORM_BWD ? p.gamma[n0 + c] : 0.f;
-  }
-  if constexpr (GST)
-    for (int m = tid; m < p.g.M; m += NT) su[m] = (BXF ? p.bop.stats : p.stats)[m];
-#pragma unroll
-  for (int nb = 0; nb < NBW; ++nb)
-#pragma unroll
-    for (int kb = 0; kb < KB; ++kb) du_ready(wf[nb][kb]);
-  asm volatile("" ::"v"(eal), "v"(bal));
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // nothing but the ring in flight from here
-  __syncthreads();
-
   // ---- col part: wave (wp, wn) owns D blocks p in [wp*64, +64), n in [n0 + wn*64, +64)
   const int wp = wid / WN, wn = wid % WN;
   f32x4_t dacc[4][4];
@@ -276,6 +259,7 @@ __global__ __launch_bounds__(DU_NT) void gemm_dual_kernel(GemmDual p) {
     brow = 8 * (wid - 4) + (lane >> 3);
     bvo = (uint32_t)(brow * p.ldr * 2 + (n0 + 8 * ((lane & 7) ^ (brow & 7))) * 2);
   }
+  auto clampt = [&](int t) __attribute__((always_inline)) { return t < t1 ? t : t1 - 1; };
   auto dma = [&](int t) __attribute__((always_inline)) {   // group of tile t -> slot t % D
     if constexpr (CTN_DU_EXP & 2) return;
     const int slot = t % D, tk = (t * TM) % Kp;
@@ -311,6 +295,42 @@ __global__ __launch_bounds__(DU_NT) void gemm_dual_kernel(GemmDual p) {
     for (int kk = kfrom; kk < k; ++kk) n += (kk >= 1 ? 1 : 0) + grp(kk + D - 1) + SST;
     return n;
   };
+
+  // CTN_DU_EARLY 0 (experiment): the first D-1 DMA groups go out before the resident
+  // weight and the constants are loaded
+  if (!CTN_DU_EARLY && t0 < t1)
+    for (int i = 0; i < D - 1; ++i)
+      if (!CTN_DU_NOCLAMP) dma(clampt(t0 + i));
+      else if (t0 + i < t1) dma(t0 + i);
+  v4u wf[NBW][KB];
+  // from the fragment-ordered copy when there is one (1 KiB contiguous per wave and
+  // fragment, as in gemm_ws)
+  const bf16raw* WF = NBW == 2 ? reinterpret_cast<const bf16raw*>(p.Wf) : nullptr;
+#pragma unroll
+  for (int nb = 0; nb < NBW; ++nb) {
+    const int n = n0 + nbg * 16 * NBW + (lr >> 2) * NV + nb * 4 + (lr & 3);
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb)
+      if constexpr (CTN_DU_EXP & 256) wf[nb][kb] = v4u{(uint32_t)n, (uint32_t)kb, 0u, 0u};   // no weight loads
+      else if (WF) wf[nb][kb] = ldg16(WF + frag_offset(sl * WNB + nbg, nb, kb, lane, KR));
+      else wf[nb][kb] = ldg16(W + (size_t)n * p.ldw + kb * 32 + lg * 8);
+  }
+  const float eal = EPI == EPI_NORM_BWD ? p.alpha[0] : 0.f;
+  const float bal = OPB == OP_PRELU_NORM ? p.bop.alpha[0] : 0.f;
+  for (int c = tid; c < NS; c += NT) {
+    sg[c] = BXF ? p.bop.gamma[n0 + c] : 0.f;
+    sg[NS + c] = BXF ? p.bop.beta[n0 + c] : 0.f;
+    sg[2 * NS + c] = EPI == EPI_NORM_BWD ? p.gamma[n0 + c] : 0.f;
+  }
+  if constexpr (GST)
+    for (int m = tid; m < p.g.M; m += NT) su[m] = (BXF ? p.bop.stats : p.stats)[m];
+#pragma unroll
+  for (int nb = 0; nb < NBW; ++nb)
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) du_ready(wf[nb][kb]);
+  asm volatile("" ::"v"(eal), "v"(bal));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // nothing but the ring in flight from here
+  __syncthreads();
 
   // ---- lane-constant LDS read addresses
   const int rbase = mbw * KB * 1024 + lg * 256 + ((lr ^ ((lg & 1) * 12)) << 4);   // + kb * 1024
@@ -504,12 +524,12 @@ __global__ __launch_bounds__(DU_NT) void gemm_dual_kernel(GemmDual p) {
     }
   };
 
-  auto clampt = [&](int t) __attribute__((always_inline)) { return t < t1 ? t : t1 - 1; };
   auto run = [&](auto le1) __attribute__((always_inline)) {
     f32x4_t acc[NBW];
-    for (int i = 0; i < D - 1; ++i)
-      if (!CTN_DU_NOCLAMP) dma(clampt(t0 + i));
-      else if (t0 + i < t1) dma(t0 + i);
+    if (CTN_DU_EARLY)
+      for (int i = 0; i < D - 1; ++i)
+        if (!CTN_DU_NOCLAMP) dma(clampt(t0 + i));
+        else if (t0 + i < t1) dma(t0 + i);
     for (int t = t0; t < t1; ++t) {
       // BXF: the transform reads raw Bm of tile t+1 this iteration, so wait for its group
       const int tq = BXF ? t + 1 : t;
@@ -556,7 +576,9 @@ __global__ __launch_bounds__(DU_NT) void gemm_dual_kernel(GemmDual p) {
     for (int j = 0; j < 4; ++j) {
       const int n = n0 + (wn * 4 + j) * 16 + lr;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) Dp[(size_t)((wp * 4 + i) * 16 + 4 * lg + e) * p.Nout + n] = dacc[i][j][e];
+      for (int e = 0; e < 4; ++e)
+        if constexpr (CTN_DU_EXP & 512) asm volatile("" ::"v"(dacc[i][j][e]));   // timing: no D partial stores
+        else Dp[(size_t)((wp * 4 + i) * 16 + 4 * lg + e) * p.Nout + n] = dacc[i][j][e];
     }
 }
 

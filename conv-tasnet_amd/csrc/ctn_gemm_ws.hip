@@ -48,7 +48,8 @@ constexpr int WS_DR = CTN_WS_DR;
 constexpr int WS_FOLD_MAX = 512;   // utterances whose gLN operand stats a workgroup holds in LDS
 
 // Bound-finding experiments only (tools/microbench): bit 0 drops the output
-// stores, bit 1 the A-tile loads, bit 2 the MFMAs, bit 3 the epilogue math; bit 6
+// stores, bit 1 the A-tile loads, bit 2 the MFMAs, bit 3 the epilogue math, bit 7 the
+// resident weight's loads; bit 6
 // (experiment, not bound-finding) lets the scheduler move epilogue math into the MFMAs.
 #ifndef CTN_WS_EXP
 #define CTN_WS_EXP 0
@@ -89,6 +90,11 @@ constexpr int WS_FOLD_MAX = 512;   // utterances whose gLN operand stats a workg
 #endif
 #if CTN_WS_STAMP
 __device__ unsigned long long ws_stamps[256 * 16 * 8];
+#endif
+// 1: wait for the resident weight before the first tiles' loads are issued; 0
+// (experiment): after them.  Measured the same.
+#ifndef CTN_WS_EARLY
+#define CTN_WS_EARLY 1
 #endif
 #ifndef CTN_WS_ORDER
 #define CTN_WS_ORDER 1
@@ -163,16 +169,36 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
   const int colbase = n0 + wid * 16 * NB + lg * NV;  // this lane's NV contiguous output channels
   const int wslot = sl * WV + wid;                    // partial-statistics column of this wave
 
-  // ---- resident weight: fragment (nb, kb), MFMA row lr -> output channel
+  // ---- resident weight: fragment (nb, kb), MFMA row lr -> output channel.  From the
+  // fragment-ordered copy when the caller made one (1 KiB contiguous per wave and
+  // fragment: half the L2 lines of the row-major reads, whose 64-byte row pieces fill
+  // only half of each line; every CU reads the whole weight, so this read is a fixed
+  // cost of the launch, 12.9 -> 7.8 us at one tile per workgroup)
   v4u wf[NB][KB];
+  const bf16raw* WF = NB == 2 ? reinterpret_cast<const bf16raw*>(p.Wf) : nullptr;
+  if (WF) {
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) wf[nb][kb] = ldg16(WF + frag_offset(sl * WV + wid, nb, kb, lane, KR));
+  } else {
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
     const int n = wid * 16 * NB + (lr >> 2) * NV + nb * 4 + (lr & 3);
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb)
-      wf[nb][kb] = ldg16(W + (size_t)n * p.ldw + kb * 32 + lg * 8);
+      if constexpr (CTN_WS_EXP & 128) wf[nb][kb] = v4u{(uint32_t)n, (uint32_t)kb, 0u, 0u};   // no weight loads
+      else if constexpr (CTN_WS_EXP & 768) {   // timing only (wrong values): contiguous / rotated
+        const int kr = (CTN_WS_EXP & 512) ? (kb + (int)blockIdx.x) % KB : kb;
+        if constexpr (CTN_WS_EXP & 256) wf[nb][kb] = ldg16(W + ((size_t)((wid * NB + nb) * KB + kr) * 64 + lane) * 8);
+        else wf[nb][kb] = ldg16(W + (size_t)n * p.ldw + kr * 32 + lg * 8);
+      } else wf[nb][kb] = ldg16(W + (size_t)n * p.ldw + kb * 32 + lg * 8);
+  }
   }
 
+  // operand statistics into LDS (FOLDS); called after the first tiles' loads are
+  // issued where the pipeline allows, so the fold's round trip overlaps them
+  auto fold_stats = [&]() __attribute__((always_inline)) {
   if constexpr (FOLDS) {
     const StatFold& f = p.aop.fold;
     if (f.slab) {
@@ -194,6 +220,7 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
       for (int gi = tid; gi < p.g.M; gi += NT) sst1[gi] = p.aop.stats[gi];
     __syncthreads();
   }
+  };
 
   // ---- A staging: thread owns k-chunk kc (fixed) of rows rl0 + j*RSTEP
   const int kc = tid % CPR, rl0 = tid / CPR;
@@ -506,17 +533,25 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
     }
   };
 
+  // wait for the resident weight and the epilogue/operand constants once, before the
+  // tile loop (CTN_WS_EARLY)
+  auto ready_all = [&]() __attribute__((always_inline)) {
 #pragma unroll
-  for (int nb = 0; nb < NB; ++nb)
+    for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
-    for (int kb = 0; kb < KB; ++kb) ready(wf[nb][kb]);
-  if constexpr (AFF) {
+      for (int kb = 0; kb < KB; ++kb) ready(wf[nb][kb]);
+    if constexpr (AFF) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { ready(og[e]); ready(ob[e]); }
+      for (int e = 0; e < 8; ++e) { ready(og[e]); ready(ob[e]); }
+    }
+    ready(oal);
+    ready(eal);
+  };
+  if constexpr (CTN_WS_EARLY) ready_all();
+  if (t0 >= t1) {
+    fold_stats();   // a workgroup without tiles still stores its utterances' pairs
+    return;
   }
-  ready(oal);
-  ready(eal);
-  if (t0 >= t1) return;
 
   // Pipeline, one LDS-only barrier per tile; tile t+1 is staged into the other LDS
   // buffer (its last reader finished before this barrier) from registers loaded an
@@ -576,7 +611,9 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
       };
       auto mn = [](int a, int b) { return a < b ? a : b; };
       f32x4_t acc[MB][NB];
+      fold_stats();
       for (int i = 0; i < WS_DR - 1; ++i) dma(t0 + i);
+      if constexpr (!CTN_WS_EARLY) ready_all();
       for (int t = t0; t < t1; ++t) {
         vmwait23(NFW * mn(WS_DR - 2, t1 - 1 - t) + SPT * mn(WS_DR - 1, t - t0));
         lds_barrier();
@@ -592,9 +629,11 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
       // prologue: tiles t0 .. t0+PF-1 into slots 0 .. PF-1; t0 staged; t0+PF into slot 0
       static_for<PF>([&](auto i) { load_a(clampt(t0 + decltype(i)::value), i); });
       load_r(t0);
+      fold_stats();
       stage(le1, t0, sA[t0 & 1], std::integral_constant<int, 0>{});
       store_gh(t0);
       load_a(clampt(t0 + PF), std::integral_constant<int, 0>{});
+      if constexpr (!CTN_WS_EARLY) ready_all();
       for (int tb = t0; tb < t1; tb += PF) {
         static_for<PF>([&](auto u) {
           constexpr int nx = (decltype(u)::value + 1) % PF;   // slot of tile t+1
@@ -633,6 +672,7 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
     } else {
       f32x4_t accP[MB][NB], accC[MB][NB];
       load_a(t0, std::integral_constant<int, 0>{});
+      fold_stats();
       stage(le1, t0, sA[t0 & 1], std::integral_constant<int, 0>{});
       load_a(clampt(t0 + 1), std::integral_constant<int, 0>{});
       lds_barrier();
@@ -640,6 +680,7 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
       load_r(t0);
       stage(le1, t0 + 1, sA[(t0 + 1) & 1], std::integral_constant<int, 0>{});
       load_a(clampt(t0 + 2), std::integral_constant<int, 0>{});
+      if constexpr (!CTN_WS_EARLY) ready_all();
       // unrolled by two so the two accumulator sets swap roles without copies
       auto step = [&](int t, f32x4_t (&cur)[MB][NB], f32x4_t (&prev)[MB][NB]) __attribute__((always_inline)) {
         lds_barrier();

@@ -46,6 +46,7 @@ struct GemmRows {
   int Kred, Nout;
   const void* A; int lda;
   const void* W; int ldw;      // [Nout][Kred], storage type
+  const void* Wf;              // optional bf16 copy of W in MFMA fragment order (frag_offset)
   RowOp aop;
   int epi = EPI_STORE;
   void* C; int ldc;
@@ -99,6 +100,7 @@ struct GemmDual {
   int Kred, Nout;
   const void* A; int lda;
   const void* W; int ldw;
+  const void* Wf;              // optional fragment-ordered bf16 copy of W (frag_offset)
   int epi = EPI_RESID;
   void* C; int ldc;
   const void* R = nullptr; int ldr = 0;
@@ -145,7 +147,17 @@ struct PrepDesc {
   int O, I;
   void* Ws;
   void* Wt;
+  void* Wf;    // W in fragment order (O, I multiples of 32), or null
+  void* Wtf;   // the transpose [I][O] in fragment order, or null
 };
+// Fragment order of a bf16 weight W [O][I] (O, I multiples of 32): the 16-byte piece
+// that lane L of output group g (32 rows) holds as MFMA A-fragment (nb, kb) of the
+// weight-stationary kernels (2 fragments of 16 rows per group: rows g*32 + ((L&15)>>2)*8
+// + nb*4 + (L&3), columns kb*32 + (L>>4)*8 .. +8) sits at element offset
+// ((g*2 + nb)*(I/32) + kb)*512 + L*8, so every wave's fragment load is 1 KiB contiguous.
+__host__ __device__ inline long frag_offset(int g, int nb, int kb, int lane, int I) {
+  return (((long)g * 2 + nb) * (I / 32) + kb) * 512 + lane * 8;
+}
 constexpr int PREP_MAX = 64;   // descriptors per launch (kernel-argument budget)
 struct PrepBatch {
   PrepDesc d[PREP_MAX];

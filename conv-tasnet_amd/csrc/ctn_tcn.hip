@@ -921,11 +921,29 @@ __global__ __launch_bounds__(256) void prep_weight_kernel(PrepBatch pb) {
     }
     tile[r][c] = v;
   }
-  if (!Wt) return;
+  if (!Wt && !d.Wf && !d.Wtf) return;
   __syncthreads();
-  for (int i = threadIdx.x; i < PW_T * PW_T; i += 256) {
-    const int c = i / PW_T, r = i % PW_T;
-    if (r0 + r < d.O && c0 + c < d.I) st1<T>(Wt + (size_t)(c0 + c) * d.O + r0 + r, tile[r][c]);
+  if (Wt) {
+    for (int i = threadIdx.x; i < PW_T * PW_T; i += 256) {
+      const int c = i / PW_T, r = i % PW_T;
+      if (r0 + r < d.O && c0 + c < d.I) st1<T>(Wt + (size_t)(c0 + c) * d.O + r0 + r, tile[r][c]);
+    }
+  }
+  // fragment-order copies (frag_offset; O and I are multiples of 32, checked by the
+  // caller, so the tile holds whole 32x32 fragment pairs): 512 pieces of 8 per copy
+  for (int pass = 0; pass < 2; ++pass) {
+    T* F = reinterpret_cast<T*>(pass ? d.Wtf : d.Wf);
+    if (!F) continue;
+    const int Icols = pass ? d.O : d.I;     // reduction length of the copy
+    const int gb = (pass ? c0 : r0) / 32, kb0 = (pass ? r0 : c0) / 32;
+    for (int i = threadIdx.x; i < 512; i += 256) {
+      const int lane = i & 63, nb = (i >> 6) & 1, kb = (i >> 7) & 1, g = i >> 8;
+      const int n = g * 32 + ((lane & 15) >> 2) * 8 + nb * 4 + (lane & 3), k = kb * 32 + (lane >> 4) * 8;
+      if ((pass ? c0 + n >= d.I || r0 + k >= d.O : r0 + n >= d.O || c0 + k >= d.I)) continue;
+      T* dst = F + frag_offset(gb + g, nb, kb0 + kb, lane, Icols);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) st1<T>(dst + e, pass ? tile[k + e][n] : tile[n][k + e]);
+    }
   }
 }
 
@@ -944,7 +962,7 @@ hipError_t launch_prep_weights(DType dt, const PrepBatch& pb, hipStream_t s) {
 
 hipError_t launch_prep_weight(DType dt, const float* W, int O, int I, void* Ws, void* Wt, hipStream_t s) {
   PrepBatch pb{};
-  pb.d[0] = PrepDesc{W, O, I, Ws, Wt};
+  pb.d[0] = PrepDesc{W, O, I, Ws, Wt, nullptr, nullptr};
   pb.nd = 1;
   return launch_prep_weights(dt, pb, s);
 }

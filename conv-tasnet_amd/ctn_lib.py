@@ -14,7 +14,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CTN_HIP_LIB", os.path.join(_HERE, "libctn_hip.so"))
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 DTYPE_F32, DTYPE_BF16 = 0, 1
 NORM_GLN, NORM_CLN, NORM_BN = 0, 1, 2
@@ -43,11 +43,13 @@ class TBlockParams(ctypes.Structure):
     _fields_ = ([(n, c_void_p) for n in _TB_PARAM_NAMES + ("w1_bf16", "w2_bf16", "w1t_bf16", "w2t_bf16",
                                                            "bn_mean1", "bn_var1", "bn_mean2", "bn_var2")] +
                 [("bn_training", c_int32), ("bn_momentum1", ctypes.c_float), ("bn_momentum2", ctypes.c_float),
-                 ("bn_eps1", ctypes.c_float), ("bn_eps2", ctypes.c_float)])
+                 ("bn_eps1", ctypes.c_float), ("bn_eps2", ctypes.c_float)] +
+                [(n, c_void_p) for n in ("w1_frag", "w2_frag", "w1t_frag", "w2t_frag")])
 
 
 class WeightPack(ctypes.Structure):
-    _fields_ = [("src", c_void_p), ("rows", c_int32), ("cols", c_int32), ("dst", c_void_p), ("dst_t", c_void_p)]
+    _fields_ = [("src", c_void_p), ("rows", c_int32), ("cols", c_int32), ("dst", c_void_p), ("dst_t", c_void_p),
+                ("dst_frag", c_void_p), ("dst_t_frag", c_void_p)]
 
 
 class TBlockGrads(ctypes.Structure):

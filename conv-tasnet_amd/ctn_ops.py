@@ -4,6 +4,7 @@ layout [M*Kp, C]; parameters stay fp32 in reference shapes."""
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 
 import torch
@@ -38,7 +39,9 @@ def _f32(t: torch.Tensor) -> torch.Tensor:
 # ----------------------------------------------------------------------------
 class WeightPacks:
     """bf16 compute copies of the TemporalBlocks' 1x1 weights (W1 [H,B], W2 [B,H]
-    and both transposes), refreshed for all stale blocks in ONE native call per
+    and both transposes, row-major and, when B and H are multiples of 32, in the
+    MFMA fragment order the weight-stationary kernels load from: include/ctn.h
+    ctn_weight_pack), refreshed for all stale blocks in ONE native call per
     step (ctn_pack_weights) instead of a conversion inside every block call.
     A copy is stale when its fp32 parameter's version counter moved: every
     in-place update bumps it (torch optimizers, load_state_dict, and
@@ -51,30 +54,36 @@ class WeightPacks:
         self.ptrs = []
 
     def get(self, pairs: list, device) -> list:
-        """pairs: [(w1, w2)] fp32 parameters -> [(w1s, w2s, w1t, w2t, buf)]: four device
-        pointers into ``buf``, returned WITH the buffer so that every autograd node
-        that saves a pack keeps its storage alive until its backward has run (the
+        """pairs: [(w1, w2)] fp32 parameters -> [(w1s, w2s, w1t, w2t, w1f, w2f, w1tf, w2tf,
+        buf)]: eight device pointers into ``buf`` (the fragment-order four None when B
+        or H is not a multiple of 32), returned WITH the buffer so that every autograd
+        node that saves a pack keeps its storage alive until its backward has run (the
         cache may reallocate ``buf`` between forward and backward)."""
         key = (device, tuple((w1.data_ptr(), w2.data_ptr(), tuple(w1.shape), tuple(w2.shape)) for w1, w2 in pairs))
         if key != self.key:
-            sizes = [(w1.numel(), w2.numel()) for w1, w2 in pairs]
-            total = sum(2 * (a + b) for a, b in sizes)
+            frag = os.environ.get("CTN_WEIGHT_FRAG", "1") != "0"   # 0: row-major copies only (A/B)
+            sizes = [(w1.numel(), w2.numel(), frag and w1.shape[0] % 32 == 0 and w1.shape[1] % 32 == 0)
+                     for w1, w2 in pairs]
+            total = sum((4 if fr else 2) * (a + b) for a, b, fr in sizes)
             self.buf = torch.empty(total, dtype=torch.bfloat16, device=device)
             base, off, self.ptrs = self.buf.data_ptr(), 0, []
-            for a, b in sizes:
-                w1s, w2s, w1t, w2t = (base + 2 * o for o in (off, off + a, off + a + b, off + 2 * a + b))
-                self.ptrs.append((w1s, w2s, w1t, w2t))
-                off += 2 * (a + b)
+            for a, b, fr in sizes:
+                n = 2 if fr else 1
+                ptrs = []
+                for _ in range(n):   # row-major (w1s, w2s, w1t, w2t), then the fragment-order four
+                    ptrs += [base + 2 * o for o in (off, off + a, off + a + b, off + 2 * a + b)]
+                    off += 2 * (a + b)
+                self.ptrs.append(tuple(ptrs) + (None,) * (8 - len(ptrs)))
             self.key = key
             self.vers = [None] * len(pairs)
         packs = []
         for i, (w1, w2) in enumerate(pairs):
             v = (w1._version, w2._version)
             if self.vers[i] != v:
-                w1s, w2s, w1t, w2t = self.ptrs[i]
+                w1s, w2s, w1t, w2t, w1f, w2f, w1tf, w2tf = self.ptrs[i]
                 H, B = w1.shape[0], w1.shape[1]
-                packs.append(L.WeightPack(_f32(w1).data_ptr(), H, B, w1s, w1t))
-                packs.append(L.WeightPack(_f32(w2).data_ptr(), B, H, w2s, w2t))
+                packs.append(L.WeightPack(_f32(w1).data_ptr(), H, B, w1s, w1t, w1f, w1tf))
+                packs.append(L.WeightPack(_f32(w2).data_ptr(), B, H, w2s, w2t, w2f, w2tf))
                 self.vers[i] = v
         if packs:
             arr = (L.WeightPack * len(packs))(*packs)
@@ -129,7 +138,8 @@ def bn_state(bn1: torch.nn.BatchNorm1d, bn2: torch.nn.BatchNorm1d) -> tuple:
 class TBlockFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, fr: Frames, cfg: tuple, pack, bn, w1, a1, g1, b1, wd, a2, g2, b2, w2):
-        """pack: (w1s, w2s, w1t, w2t) bf16 copies from WeightPacks, or None.
+        """pack: (w1s, w2s, w1t, w2t, w1f, w2f, w1tf, w2tf, buf) bf16 copies from
+        WeightPacks, or None.
         bn: BatchNorm state for norm_type BN (bn_state()), else None."""
         B, H, P, dil, causal, norm = cfg
         lib = L.load()
@@ -138,9 +148,10 @@ class TBlockFn(torch.autograd.Function):
         params = [_f32(t) for t in (w1, a1, g1, b1, wd, a2, g2, b2, w2)]
         desc = L.TBlockDesc(fr.M, fr.K, fr.Kp, B, H, P, dil, int(causal), norm, L.dtype_code(x.dtype))
         pack = pack if x.dtype == torch.bfloat16 else None
-        ctx.pack = pack          # (4 pointers, buf): keeps the packed storage alive until backward
+        ctx.pack = pack          # (8 pointers, buf): keeps the packed storage alive until backward
         ctx.bn = bn or _NO_BN
-        pstruct = L.TBlockParams(*[p.data_ptr() for p in params], *(pack[:4] if pack else (None,) * 4), *ctx.bn)
+        pstruct = L.TBlockParams(*[p.data_ptr() for p in params], *(pack[:4] if pack else (None,) * 4), *ctx.bn,
+                                 *(pack[4:8] if pack else (None,) * 4))
         y = torch.empty_like(x)
         h1 = x.new_empty(fr.rows, H)
         d = x.new_empty(fr.rows, H)
@@ -165,7 +176,7 @@ class TBlockFn(torch.autograd.Function):
             gy = gy.to(x.dtype)
         desc = L.TBlockDesc(*ctx.desc)
         pstruct = L.TBlockParams(*[p.data_ptr() for p in params], *(ctx.pack[:4] if ctx.pack else (None,) * 4),
-                                 *ctx.bn)
+                                 *ctx.bn, *(ctx.pack[4:8] if ctx.pack else (None,) * 4))
         saved = L.TBlockSaved(h1.data_ptr(), d.data_ptr(), stats.data_ptr())
         gx = torch.empty_like(x)
         grads = [torch.empty_like(p) for p in params]

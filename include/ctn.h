@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define CTN_ABI_VERSION 5
+#define CTN_ABI_VERSION 6
 
 typedef enum { CTN_DTYPE_F32 = 0, CTN_DTYPE_BF16 = 1 } ctn_dtype;
 /* CTN_NORM_BN: torch.nn.BatchNorm1d, chose_norm's fallback branch (conv_tasnet.py:302-303) */
@@ -94,15 +94,28 @@ typedef struct {            /* fp32 device pointers, reference shapes */
   int32_t bn_training;      /* 1: batch statistics (train mode), 0: running statistics */
   float bn_momentum1, bn_momentum2;
   float bn_eps1, bn_eps2;
+  /* optional (ABI v6, dtype BF16, B and H multiples of 32): the same four bf16 copies in
+   * MFMA fragment order (ctn_weight_pack dst_frag / dst_t_frag), from which the
+   * weight-stationary kernels load their resident weight 1 KiB contiguous per wave;
+   * NULL: they read the row-major copies above */
+  const void* w1_frag;
+  const void* w2_frag;
+  const void* w1t_frag;
+  const void* w2t_frag;
 } ctn_tblock_params;
 
 /* One fp32 weight [rows][cols] -> bf16 copy (dst, same layout) and/or bf16
- * transpose (dst_t, [cols][rows]); either may be NULL. */
+ * transpose (dst_t, [cols][rows]), and (ABI v6) the same two in MFMA fragment order
+ * (dst_frag, dst_t_frag; rows and cols multiples of 32): element (n, k) of a [O][I]
+ * matrix at ((g*2 + nb)*(I/32) + kb)*512 + lane*8 + e for n = g*32 + ((lane&15)>>2)*8
+ * + nb*4 + (lane&3), k = kb*32 + (lane>>4)*8 + e.  Any destination may be NULL. */
 typedef struct {
   const float* src;
   int32_t rows, cols;
   void* dst;
   void* dst_t;
+  void* dst_frag;
+  void* dst_t_frag;
 } ctn_weight_pack;
 /* Converts n weights in ceil(n / 64) launches (a training step's bf16 weight
  * copies for all TemporalBlocks at once, instead of per block call). */

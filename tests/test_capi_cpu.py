@@ -104,3 +104,18 @@ def test_timer_off_by_default(lib):
     tot, n = ctypes.c_double(1.0), ctypes.c_int(7)
     assert lib.ctn_timer_read(ctypes.byref(tot), ctypes.byref(n)) == 0
     assert n.value == 0 and tot.value == 0.0
+
+
+def test_pack_weights_validation(lib):
+    """ctn_pack_weights checks its table before launching anything: an entry needs a
+    destination, and the fragment-order copies need rows and cols in multiples of 32."""
+    import ctn_lib as L
+    assert lib.ctn_pack_weights(None, 0, None) == 0
+    empty = (L.WeightPack * 1)(L.WeightPack(16, 64, 64, None, None, None, None))
+    assert lib.ctn_pack_weights(empty, 1, None) == 1
+    assert "no destination" in lib.ctn_last_error().decode()
+    ragged = (L.WeightPack * 1)(L.WeightPack(16, 40, 64, None, None, 256, None))
+    assert lib.ctn_pack_weights(ragged, 1, None) == 1
+    assert "multiples of 32" in lib.ctn_last_error().decode()
+    ragged_t = (L.WeightPack * 1)(L.WeightPack(16, 64, 72, None, None, None, 256))
+    assert lib.ctn_pack_weights(ragged_t, 1, None) == 1

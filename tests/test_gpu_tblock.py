@@ -141,6 +141,39 @@ def test_weight_packs_match_per_call_conversion():
             ps[8].add_(0.01)
 
 
+def _frag_order(w: np.ndarray) -> np.ndarray:
+    """include/ctn.h ctn_weight_pack fragment order of W [O][I], restated with numpy:
+    flat index ((g*2 + nb)*(I/32) + kb)*512 + lane*8 + e holds
+    W[g*32 + ((lane&15)>>2)*8 + nb*4 + (lane&3)][kb*32 + (lane>>4)*8 + e]."""
+    O, I = w.shape
+    g, nb, kb, lane, e = np.meshgrid(np.arange(O // 32), np.arange(2), np.arange(I // 32), np.arange(64),
+                                     np.arange(8), indexing="ij")
+    n = g * 32 + ((lane & 15) >> 2) * 8 + nb * 4 + (lane & 3)
+    k = kb * 32 + (lane >> 4) * 8 + e
+    return w[n, k].reshape(-1)
+
+
+@pytest.mark.parametrize("O,I", [(512, 256), (256, 512), (96, 160)])
+def test_pack_weights_fragment_order(O, I):
+    """ctn_pack_weights' fragment-order copies (and their transposes) hold exactly the
+    permutation include/ctn.h documents, element for element, besides the row-major
+    bf16 copy and transpose."""
+    import ctn_lib as L
+    torch.manual_seed(0)
+    w = torch.randn(O, I, device=DEV)
+    outs = [torch.full((O * I,), float("nan"), dtype=torch.bfloat16, device=DEV) for _ in range(4)]
+    pk = (L.WeightPack * 1)(L.WeightPack(w.data_ptr(), O, I, *[t.data_ptr() for t in outs]))
+    L.check(L.load().ctn_pack_weights(pk, 1, L.stream_handle(w.device)), "ctn_pack_weights")
+    torch.cuda.synchronize()
+    wb = w.to(torch.bfloat16).cpu()
+    dst, dst_t, frag, frag_t = [t.cpu() for t in outs]
+    assert torch.equal(dst.view(O, I), wb)
+    assert torch.equal(dst_t.view(I, O), wb.t())
+    wn = wb.float().numpy()
+    assert np.array_equal(frag.float().numpy(), _frag_order(wn))
+    assert np.array_equal(frag_t.float().numpy(), _frag_order(np.ascontiguousarray(wn.T)))
+
+
 @pytest.mark.parametrize("d,causal,norm", [(2, 0, "gLN"), (32, 1, "gLN"), (2, 0, "cLN"), (32, 1, "cLN")])
 def test_dual_gemm_matches_four_kernel_path(d, causal, norm, monkeypatch):
     """The dual GEMMs (row GEMM + weight gradient in one pass, ctn_gemm_dual.hip) give

@@ -32,7 +32,8 @@ __global__ __launch_bounds__(256) void stream_kernel(const v4u* a, v4u* c, long 
 }
 
 int main() {
-  const int M = 32, K = 3199, Kp = 3200, B = 256, H = 512;
+  // DB_M: utterances (default 32; the fixed per-launch cost is the intercept over M)
+  const int M = getenv("DB_M") ? atoi(getenv("DB_M")) : 32, K = 3199, Kp = 3200, B = 256, H = 512;
   const long rows = (long)M * Kp;
   void* x = dev_fill(rows * B * 2, 1);
   void* gy = dev_fill(rows * B * 2, 5);
@@ -57,12 +58,14 @@ int main() {
     g.alpha = al; g.stats = (const float2*)st; g.gamma = gm; g.grp_slab = slab;
     g.Bm = d; g.ldb = H; g.bop.kind = OP_PRELU_NORM; g.bop.norm = g.norm; g.bop.stats = (const float2*)st;
     g.bop.gamma = gm; g.bop.beta = bt; g.bop.alpha = al; g.Dpart = dpart;
+    if (getenv("DB_FRAG")) g.Wf = w;   // timing: the fragment-order load pattern
     cs.push_back({"A: gy.W2t norm-bwd + dW2", g, rows * (B + 2 * H) * 2.0});
   }
   {
     GemmDual g{}; g.g = Rows{M, K, Kp}; g.Kred = H; g.Nout = B; g.norm = NORM_GLN;
     g.A = d; g.lda = H; g.W = w; g.ldw = H; g.C = out; g.ldc = B; g.epi = EPI_RESID; g.R = gy; g.ldr = B;
     g.Bm = x; g.ldb = B; g.Dpart = dpart;
+    if (getenv("DB_FRAG")) g.Wf = w;
     cs.push_back({"B: gh1.W1t + gy + dW1", g, rows * (H + 3 * B) * 2.0});
   }
   hipEvent_t e0, e1;
@@ -77,7 +80,7 @@ int main() {
     CK(hipEventSynchronize(e1));
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
     const double us = ms * 1e3 / NIT;
-    printf("EXP %3d  %-30s %8.1f us  %7.0f GB/s\n", CTN_DU_EXP, c.name, us, c.bytes / us * 1e-3);
+    printf("EXP %3d M=%d  %-30s %8.1f us  %7.0f GB/s\n", CTN_DU_EXP, M, c.name, us, c.bytes / us * 1e-3);
 #if CTN_DU_STAMP
     {   // per-phase shares of the loop (diagnostic build: read shares, not lengths)
       std::vector<unsigned long long> h(DU_GRID * DU_WV * 8);
@@ -102,7 +105,7 @@ int main() {
     CK(hipEventSynchronize(e1));
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
     const double us = ms * 1e3 / NIT;
-    printf("stream copy (%ld MB read, %ld MB written) %8.1f us %7.0f GB/s\n", n * 16 >> 20, n * 16 >> 20, us,
+    printf("M=%d stream copy (%ld MB read, %ld MB written) %8.1f us %7.0f GB/s\n", M, n * 16 >> 20, n * 16 >> 20, us,
            2.0 * n * 16 / us * 1e-3);
   }
   return 0;

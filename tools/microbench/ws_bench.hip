@@ -32,7 +32,8 @@ __global__ __launch_bounds__(256) void stream_kernel(const v4u* a, v4u* c, long 
 }
 
 int main() {
-  const int M = 32, K = 3199, Kp = 3200, B = 256, H = 512;
+  // WSB_M: utterances (default 32; the fixed per-launch cost is the intercept over M)
+  const int M = getenv("WSB_M") ? atoi(getenv("WSB_M")) : 32, K = 3199, Kp = 3200, B = 256, H = 512;
   const long rows = (long)M * Kp;
   void* x = dev_fill(rows * B * 2, 1);
   void* d = dev_fill(rows * H * 2, 2);
@@ -50,7 +51,9 @@ int main() {
   struct Case { const char* name; GemmRows g; double bytes; };
   std::vector<Case> cs;
   auto base = [&](int Kred, int Nout) { GemmRows g{}; g.g = Rows{M, K, Kp}; g.Kred = Kred; g.Nout = Nout; g.norm = NORM_GLN;
-    g.lda = Kred; g.ldw = Kred; g.ldc = Nout; g.alpha = al; g.grp_slab = slab; g.W = w; return g; };
+    g.lda = Kred; g.ldw = Kred; g.ldc = Nout; g.alpha = al; g.grp_slab = slab; g.W = w;
+    if (getenv("WSB_FRAG")) g.Wf = w;   // timing: the fragment-order load pattern (values not meaningful)
+    return g; };
   { GemmRows g = base(B, H); g.A = x; g.C = out; g.epi = EPI_PRELU_STATS; cs.push_back({"fwd1 x.W1 prelu-stats", g, rows * (B + H) * 2.0}); }
   { GemmRows g = base(H, B); g.A = d; g.C = out; g.epi = EPI_RESID; g.R = x; g.ldr = B;
     g.aop.kind = OP_PRELU_NORM; g.aop.norm = NORM_GLN; g.aop.stats = (const float2*)st; g.aop.gamma = gm; g.aop.beta = bt; g.aop.alpha = al;
@@ -79,6 +82,7 @@ int main() {
                      {"stream r105MB w0", rows * H * 2, 0}, {"stream r0 w105MB", 0, rows * H * 2}};
     for (const auto& c : sc) {
       for (int grid : {1024, 4096}) {
+      if (getenv("WSB_NOSTREAM")) break;
         for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(stream_kernel, dim3(grid), dim3(256), 0, 0, (const v4u*)d, (v4u*)out, c.rd / 16, c.wr / 16);
         CK(hipDeviceSynchronize());
         CK(hipEventRecord(e0, 0));
@@ -105,7 +109,7 @@ int main() {
     CK(hipEventSynchronize(e1));
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
     const double us = ms * 1e3 / reps;
-    printf("EXP=%d  %-24s %8.1f us  %7.0f GB/s (alg)\n", CTN_WS_EXP, c.name, us, c.bytes / (us * 1e-6) / 1e9);
+    printf("EXP=%d M=%d  %-24s %8.1f us  %7.0f GB/s (alg)\n", CTN_WS_EXP, M, c.name, us, c.bytes / (us * 1e-6) / 1e9);
 #if CTN_WS_STAMP
     {   // per-phase shares of the loop (diagnostic build: read shares, not lengths)
       std::vector<unsigned long long> h(256 * 16 * 8, 0ull);
