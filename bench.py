@@ -248,6 +248,9 @@ def main():
     torch.manual_seed(0)
     model = ct.ConvTasNet(**cfg).to(dev)
     model.act_dtype = torch.float32 if args.fp32 else torch.bfloat16
+    # parameter-gradient tails on a second stream (ctn_ops._split_ok): off, the overlap
+    # slowed the step by 6 % at this batch; CTN_WGRAD_STREAM=1 for A/B
+    model.wgrad_stream = os.environ.get("CTN_WGRAD_STREAM", "0") == "1"
     if use_ddp:
         # gradients as views into the RCCL buckets (no per-step copy into the buckets),
         # one fixed graph (the reducer skips its unused-parameter search each step)

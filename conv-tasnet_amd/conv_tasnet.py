@@ -83,6 +83,12 @@ class ConvTasNet(nn.Module):
             if p.dim() > 1:
                 nn.init.xavier_normal_(p)
         self.act_dtype = None     # None: follow autocast; or torch.float32 / torch.bfloat16
+        # True: in a plain .backward() with no gradients yet, each TemporalBlock's
+        # parameter-gradient tail runs on a second stream and writes .grad directly,
+        # overlapping the next block's backward (ctn_ops._split_ok lists the conditions;
+        # otherwise the one-stream path runs).  Off by default: at the paper batch the
+        # overlapped kernels slow each other down more than the overlap saves (§11).
+        self.wgrad_stream = False
 
     def forward(self, mixture):
         """mixture [M, T] -> est_source [M, C, T] (conv_tasnet.py:45-60)."""
@@ -103,8 +109,9 @@ class ConvTasNet(nn.Module):
             if not hasattr(self, "_packs"):
                 self._packs = ops.PackCache()
             packs = self._packs.get([(b.net[0].weight, b._params()[8]) for b in blocks], mixture.device)
+        split = self.wgrad_stream and torch.is_grad_enabled()
         for blk, pk in zip(blocks, packs):
-            x = blk._forward_rows(x, fr, norm, pk)
+            x = blk._forward_rows(x, fr, norm, pk, split)
         return ops.DecoderFn.apply(x, w_rows, fr, (T, self.N, self.L, self.B, self.C, _mask_code(self.mask_nonlinear)),
                                    sep.network[3].weight, self.decoder.basis_signals.weight)
 
@@ -268,10 +275,10 @@ class TemporalBlock(nn.Module):
         return (self.net[0].weight, self.net[1].weight, g1, b1, ds[0].weight,
                 ds[1 + off].weight, g2, b2, ds[3 + off].weight)
 
-    def _forward_rows(self, x_rows, fr, norm, pack=None):
+    def _forward_rows(self, x_rows, fr, norm, pack=None, wgrad_split=False):
         B, H, P, dil, causal, _ = self._geo
         bn = ops.bn_state(*self._norms()) if norm == L.NORM_BN else None
-        return ops.TBlockFn.apply(x_rows, fr, (B, H, P, dil, causal, norm), pack, bn, *self._params())
+        return ops.TBlockFn.apply(x_rows, fr, (B, H, P, dil, causal, norm, wgrad_split), pack, bn, *self._params())
 
     def forward(self, x):
         """x [M, B, K] -> [M, B, K]."""

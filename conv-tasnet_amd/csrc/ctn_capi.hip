@@ -632,16 +632,47 @@ extern "C" int ctn_tblock_forward(const ctn_tblock_desc* d, const ctn_tblock_par
   return CTN_OK;
 }
 
+// one fork event per device (hipStreamWaitEvent takes the event's state when it is
+// called, so re-recording it for the next call is safe)
+static hipError_t fork_stream(hipStream_t from, hipStream_t to) {
+  static hipEvent_t ev[64] = {};
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+  if (!ev[dev] && (e = hipEventCreateWithFlags(&ev[dev], hipEventDisableTiming)) != hipSuccess) return e;
+  if ((e = hipEventRecord(ev[dev], from)) != hipSuccess) return e;
+  return hipStreamWaitEvent(to, ev[dev], 0);
+}
+
+static int tb_backward(const ctn_tblock_desc* d, const ctn_tblock_params* p, const void* x,
+                       const ctn_tblock_saved* sv, const void* gy, void* gx, const ctn_tblock_grads* gr,
+                       void* ws, size_t ws_bytes, hipStream_t s, hipStream_t sw);
+
 extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_params* p, const void* x,
                                    const ctn_tblock_saved* sv, const void* gy, void* gx, const ctn_tblock_grads* gr,
                                    void* ws, size_t ws_bytes, void* stream) {
+  return tb_backward(d, p, x, sv, gy, gx, gr, ws, ws_bytes, (hipStream_t)stream, (hipStream_t)stream);
+}
+
+extern "C" int ctn_tblock_backward_split(const ctn_tblock_desc* d, const ctn_tblock_params* p, const void* x,
+                                         const ctn_tblock_saved* sv, const void* gy, void* gx,
+                                         const ctn_tblock_grads* gr, void* ws, size_t ws_bytes, void* stream,
+                                         void* wgrad_stream) {
+  return tb_backward(d, p, x, sv, gy, gx, gr, ws, ws_bytes, (hipStream_t)stream,
+                     wgrad_stream ? (hipStream_t)wgrad_stream : (hipStream_t)stream);
+}
+
+// sw: the stream of the parameter-gradient tail (== s: one stream)
+static int tb_backward(const ctn_tblock_desc* d, const ctn_tblock_params* p, const void* x,
+                       const ctn_tblock_saved* sv, const void* gy, void* gx, const ctn_tblock_grads* gr,
+                       void* ws, size_t ws_bytes, hipStream_t s, hipStream_t sw) {
   int rc = tb_check(d);
   if (rc) return rc;
   if (!p || !x || !sv || !gy || !gx || !gr) return fail(CTN_ERR_ARG, "null pointer");
-  if (d->norm_type == CTN_NORM_BN) return tb_backward_bn(d, p, x, sv, gy, gx, gr, ws, ws_bytes, (hipStream_t)stream);
+  if (d->norm_type == CTN_NORM_BN) return tb_backward_bn(d, p, x, sv, gy, gx, gr, ws, ws_bytes, s);
   const TbLayout L = tb_layout(d, 1, ws);
   if (!ws || ws_bytes < L.bytes) return fail(CTN_ERR_WORKSPACE, "workspace %zu < %zu", ws_bytes, L.bytes);
-  hipStream_t s = (hipStream_t)stream;
   const DType dt = d->dtype == CTN_DTYPE_BF16 ? BF16 : F32;
   const Rows rg{d->M, d->K, d->Kp};
   const int G = tb_groups(d);
@@ -731,13 +762,15 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
     else gb.aop.sums = L.sums1;
     CTN_HIP(launch_gemm_rows(dt, gb, s));
     nalpha = gemm_ws_grid(gb);
+    // everything below only produces parameter gradients: fork to sw
+    if (sw != s) CTN_HIP(fork_stream(s, sw));
     // (f) dW1 = gh1^T . x, gh1 = G1 as stored by the kernel above
     GemmCols c1{};
     c1.g = rg; c1.P = d->H; c1.Q = d->B;
     c1.A = L.G1; c1.lda = d->H;
     c1.B = x; c1.ldb = d->B;
     c1.Cpart = L.cpart1; c1.nchunks = L.chunks1;
-    CTN_HIP(launch_gemm_cols(dt, c1, s));
+    CTN_HIP(launch_gemm_cols(dt, c1, sw));
   } else {
     // (d) norm1 backward finish + PReLU1 backward -> G1 = dL/dh1
     DwArgs de = da;
@@ -767,6 +800,7 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
       c1.Cpart = L.cpart1; c1.nchunks = L.chunks1;
       CTN_HIP(launch_gemm_cols(dt, c1, s));
     }
+    if (sw != s) CTN_HIP(fork_stream(s, sw));
   }
   // (g) all parameter-gradient partial sums
   const int dwb = dw_blocks(da), dws = dw_col_stride(da);
@@ -782,7 +816,7 @@ extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_pa
   sb.d[7] = SlabDesc{L.colD + (4 + d->P) * H, gr->alpha2, dwb, 1, dws};
   sb.d[8] = SlabDesc{L.alphaSlab, gr->alpha1, nalpha, 1, 1};
   sb.nd = 9;
-  CTN_HIP(launch_slab_reduce(sb, L.srtmp, s));
+  CTN_HIP(launch_slab_reduce(sb, L.srtmp, sw));
   return CTN_OK;
 }
 

@@ -107,6 +107,8 @@ _SIGS = {
                                           c_void_p, c_size_t, c_void_p]),
     "ctn_tblock_backward": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                            c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "ctn_tblock_backward_split": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                                 c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p]),
     "ctn_encoder_workspace_bytes": (c_size_t, [c_void_p, ctypes.c_int]),
     "ctn_encoder_forward": (ctypes.c_int, [c_void_p] + [c_void_p] * 8 + [c_void_p, c_size_t, c_void_p]),
     "ctn_encoder_backward": (ctypes.c_int, [c_void_p] + [c_void_p] * 13 + [c_void_p, c_size_t, c_void_p]),

@@ -135,13 +135,63 @@ def bn_state(bn1: torch.nn.BatchNorm1d, bn2: torch.nn.BatchNorm1d) -> tuple:
     return (*out_ptrs, int(training), facs[0], facs[1], epss[0], epss[1])
 
 
+# ----------------------------------------------------------------------------
+# parameter gradients on a second stream (ctn_tblock_backward_split)
+# ----------------------------------------------------------------------------
+_WGRAD_STREAMS = {}
+_WGRAD_PENDING = set()
+
+
+def _wgrad_stream(device) -> torch.cuda.Stream:
+    st = _WGRAD_STREAMS.get(device)
+    if st is None:
+        st = _WGRAD_STREAMS.setdefault(device, torch.cuda.Stream(device=device))
+    return st
+
+
+def _join_wgrad(device):
+    """End of the backward pass: the caller's stream waits for the parameter-gradient
+    stream, so every consumer of .grad (clip, optimizer, user code) sees them done."""
+    _WGRAD_PENDING.discard(device)
+    torch.cuda.current_stream(device).wait_stream(_wgrad_stream(device))
+
+
+def _split_ok(ctx) -> bool:
+    """The parameter-gradient tail may run on the side stream and write .grad directly
+    only when nothing can observe the gradients before the backward pass ends: a plain
+    .backward() that will accumulate into every one of these leaves (not
+    autograd.grad), no gradient yet (no accumulation), no hooks, fp32 contiguous
+    leaves, no torch.distributed (DDP hooks read gradients as they arrive)."""
+    if not ctx.wgrad_split or torch.is_grad_enabled():
+        return False
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
+        return False
+    for p, node in zip(ctx.param_refs, ctx.acc_nodes):
+        if (node is None or p.grad is not None or p.dtype != torch.float32 or not p.is_contiguous()
+                or p._backward_hooks or getattr(p, "_post_accumulate_grad_hooks", None)):
+            return False
+        try:
+            if not torch._C._will_engine_execute_node(node):
+                return False
+        except RuntimeError:   # autograd.grad() with these leaves as inputs
+            return False
+    return True
+
+
 class TBlockFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, fr: Frames, cfg: tuple, pack, bn, w1, a1, g1, b1, wd, a2, g2, b2, w2):
         """pack: (w1s, w2s, w1t, w2t, w1f, w2f, w1tf, w2tf, buf) bf16 copies from
         WeightPacks, or None.
-        bn: BatchNorm state for norm_type BN (bn_state()), else None."""
-        B, H, P, dil, causal, norm = cfg
+        bn: BatchNorm state for norm_type BN (bn_state()), else None.
+        cfg[6] (optional, ConvTasNet.wgrad_stream): let the backward run its
+        parameter-gradient tail on a second stream when that is unobservable (_split_ok)."""
+        B, H, P, dil, causal, norm = cfg[:6]
+        ctx.wgrad_split = len(cfg) > 6 and bool(cfg[6])
+        if ctx.wgrad_split:
+            ctx.param_refs = (w1, a1, g1, b1, wd, a2, g2, b2, w2)
+            ctx.acc_nodes = tuple(torch.autograd.graph.get_gradient_edge(t).node if t.requires_grad and t.is_leaf
+                                  else None for t in ctx.param_refs)
         lib = L.load()
         L.require_device(x, "TemporalBlock")
         x = x.contiguous()
@@ -183,11 +233,30 @@ class TBlockFn(torch.autograd.Function):
         gstruct = L.TBlockGrads(*[g.data_ptr() for g in grads])
         nb = lib.ctn_tblock_workspace_bytes(ctypes.byref(desc), 1)
         ws = L.workspace(nb, x.device)
-        L.check(lib.ctn_tblock_backward(ctypes.byref(desc), ctypes.byref(pstruct), x.data_ptr(),
-                                        ctypes.byref(saved), gy.data_ptr(), gx.data_ptr(), ctypes.byref(gstruct),
-                                        ws.data_ptr(), nb, L.stream_handle(x.device)),
-                "ctn_tblock_backward")
-        return (gx, None, None, None, None, *grads)
+        if not _split_ok(ctx):
+            L.check(lib.ctn_tblock_backward(ctypes.byref(desc), ctypes.byref(pstruct), x.data_ptr(),
+                                            ctypes.byref(saved), gy.data_ptr(), gx.data_ptr(), ctypes.byref(gstruct),
+                                            ws.data_ptr(), nb, L.stream_handle(x.device)),
+                    "ctn_tblock_backward")
+            return (gx, None, None, None, None, *grads)
+        # the dW1 GEMM and the parameter-gradient reductions overlap the next block's
+        # backward on the side stream; they read x and ws and write the gradients, whose
+        # memory the caching allocator must not hand out again before they finish
+        side = _wgrad_stream(x.device)
+        L.check(lib.ctn_tblock_backward_split(ctypes.byref(desc), ctypes.byref(pstruct), x.data_ptr(),
+                                              ctypes.byref(saved), gy.data_ptr(), gx.data_ptr(),
+                                              ctypes.byref(gstruct), ws.data_ptr(), nb, L.stream_handle(x.device),
+                                              side.cuda_stream),
+                "ctn_tblock_backward_split")
+        for t in (x, ws, *grads):
+            t.record_stream(side)
+        for p, g in zip(ctx.param_refs, grads):
+            p.grad = g
+        if x.device not in _WGRAD_PENDING:
+            _WGRAD_PENDING.add(x.device)
+            dev = x.device
+            torch.autograd.Variable._execution_engine.queue_callback(lambda: _join_wgrad(dev))
+        return (gx, None, None, None, None) + (None,) * 9
 
 
 # ----------------------------------------------------------------------------

@@ -138,6 +138,17 @@ int ctn_tblock_forward(const ctn_tblock_desc* d, const ctn_tblock_params* p, con
 int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_params* p, const void* x,
                         const ctn_tblock_saved* saved, const void* gy, void* gx,
                         const ctn_tblock_grads* g, void* ws, size_t ws_bytes, void* stream);
+/* ABI v6: the same backward with its parameter-gradient tail on a second stream.  The
+ * data-gradient chain (gx) is queued on `stream`; the first 1x1 conv's weight-gradient
+ * GEMM and all parameter-gradient reductions wait for an event recorded on `stream`
+ * once their inputs exist and run on `wgrad_stream`, so they overlap the previous
+ * block's backward on `stream`.  The caller keeps x, ws and the gradient outputs alive
+ * and unmodified until `wgrad_stream` has finished this call's work, and orders the
+ * consumers of g after it (norm_type BN: everything on `stream`). */
+int ctn_tblock_backward_split(const ctn_tblock_desc* d, const ctn_tblock_params* p, const void* x,
+                              const ctn_tblock_saved* saved, const void* gy, void* gx,
+                              const ctn_tblock_grads* g, void* ws, size_t ws_bytes, void* stream,
+                              void* wgrad_stream);
 
 /* -------------------------------------------------------------------------
  * Front of the network: Encoder (src/conv_tasnet.py:97-117: ReLU(Conv1d(1,N,L,
