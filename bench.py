@@ -306,11 +306,15 @@ def main():
         kb = kernel_bytes(args.timer_kind, M, K, cfg, s)
         mean_ms = tot.value / max(nl.value, 1)
         achieved = kb / (mean_ms * 1e-3) / 1e9
-        traffic = mfma = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc):
+        traffic = mfma = step_pmc = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")   # c2 FETCH_SIZE/WRITE_SIZE passes
+        if os.path.exists(pmc) and args.config == "c2":
             with open(pmc) as f:
                 traffic = json.load(f).get(str(args.timer_kind))
+        pmc = os.path.join(ROOT, "profiles", "pmc_step.json")      # the same passes, whole step (tools/pmc_step.py)
+        if os.path.exists(pmc) and args.config == "c2" and not args.fp32:
+            with open(pmc) as f:
+                step_pmc = json.load(f).get("step_GB")
         pmc = os.path.join(ROOT, "profiles", "pmc_mfma.json")   # tools/gpu_round2.sh MFMA pass
         if os.path.exists(pmc):
             with open(pmc) as f:
@@ -352,7 +356,9 @@ def main():
                          "step_frac": round(step_alg_bytes(M, K, T, cfg, s) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
             "step_model": {"alg_bytes_GB": round(step_alg_bytes(M, K, T, cfg, s) / 1e9, 3),
                            "alg_GBps": round(step_alg_bytes(M, K, T, cfg, s) / (ms * 1e-3) / 1e9, 1),
-                           "tflops": round(step_flops(M, K, cfg) / (ms * 1e-3) / 1e12, 1)},
+                           "tflops": round(step_flops(M, K, cfg) / (ms * 1e-3) / 1e12, 1),
+                           # HBM bytes of one whole step measured by rocprofv3 (committed PMC passes)
+                           "pmc_GB": round(step_pmc, 2) if step_pmc else None},
             "final_loss": round(final_loss, 4),
         }
         if world == 1 and not args.no_cpu_baseline:
