@@ -320,7 +320,8 @@ def main():
             with open(pmc) as f:
                 mfma = json.load(f).get(str(args.timer_kind))
         out = {
-            "metric": "utterances/sec (4s, 8kHz, 2-spk) fwd+bwd",
+            "metric": ("utterances/sec (4s, 8kHz, 2-spk) fwd+bwd" if args.config == "c2" else
+                       f"utterances/sec ({args.seconds:g}s, {rate // 1000}kHz, {C}-spk) fwd+bwd, {args.config}"),
             "value": round(utt_s, 2),
             "unit": "utterances/sec",
             "n_gpus": world,

@@ -21,6 +21,10 @@ namespace ctn {
 #ifndef CTN_DW_PF
 #define CTN_DW_PF 2
 #endif
+// dw_bwd, cLN: per-row statistics of 64 walk steps per lane, broadcast by v_readlane
+#ifndef CTN_DW_BATCH
+#define CTN_DW_BATCH 1
+#endif
 constexpr int DW_RPB = 128;   // rows per workgroup (element-wise kernels)
 constexpr int DW_MAXP = 8;
 constexpr int DW_MINSEG = 16; // shortest comb segment (halo rows cost (P-1)/seg)
@@ -369,9 +373,27 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
     rd.load(dd + (size_t)row * H + c * 8);
     rg.load(ga2 + (size_t)row * H + c * 8);
   };
+  // cLN with one comb item per wave: the per-row statistics of 64 consecutive walk steps
+  // are loaded one step per lane and broadcast with v_readlane, instead of a dependent
+  // global load in front of every row (bstep: the step being finished, -1 outside the walk)
+  float2 bst2 = make_float2(0.f, 0.f), bsm2 = bst2, bst1 = bst2;
+  int bbase = -(1 << 29), bstep = -1;
+  auto bl = [&](int jj) { const int k = row_of(jj); return it.base + ((jj >= 0 && k < K) ? k : 0); };
+  auto batch_load = [&](int jb) {
+    bbase = jb;
+    const int rgw = bl(jb + (threadIdx.x & 63) + GT), rhw = bl(jb + (threadIdx.x & 63) + AT);
+    bst2 = a.st2[rgw];
+    bsm2 = a.sm2[rgw];
+    bst1 = a.st1[rhw];
+  };
+  auto bcast = [&](float2 v) {
+    const int l = __builtin_amdgcn_readfirstlane(bstep - bbase);
+    return make_float2(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.x), l)),
+                       __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.y), l)));
+  };
   auto finish_g = [&](const Raw8<T>& rd, const Raw8<T>& rg, bool ok, int row, bool count, f32x2_t* gd) {
-    const float2 st = NK == NORM_GLN ? st2u : a.st2[row];
-    const float2 sm = NK == NORM_GLN ? sm2u : a.sm2[row];
+    const float2 st = NK == NORM_GLN ? st2u : (bstep >= 0 ? bcast(bst2) : a.st2[row]);
+    const float2 sm = NK == NORM_GLN ? sm2u : (bstep >= 0 ? bcast(bsm2) : a.sm2[row]);
     const f32x2_t nm = {-st.x, -st.x}, nsx = {-sm.x, -sm.x}, nsy = {-sm.y, -sm.y};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -398,7 +420,7 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
     rh.load(h1 + (size_t)row * H + c * 8);
   };
   auto finish_h = [&](const Raw8<T>& rh, int row, f32x2_t* ah) {
-    const float2 st = NK == NORM_GLN ? st1u : a.st1[row];
+    const float2 st = NK == NORM_GLN ? st1u : (bstep >= 0 ? bcast(bst1) : a.st1[row]);
     const f32x2_t nm = {-st.x, -st.x};
 #pragma unroll
     for (int i = 0; i < 4; ++i) ah[i] = (pr2(f32x2_t{rh[2 * i], rh[2 * i + 1]}, al1) + nm) * st.y;
@@ -566,6 +588,12 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
     if (j + D < it.j1) {
       fetch_g(j + D + GT, pd[q], pg[q], pok[q], prow[q]);
       fetch_h(j + D + AT, ph[q], pokh[q], prowh[q]);
+    }
+    if constexpr (NK != NORM_GLN && CTN_DW_BATCH) {
+      if (wave_item) {
+        if (j - bbase >= 64) batch_load(j);
+        bstep = j;
+      }
     }
     body(j, cd, cgv, ch, cok, cokh, crow, crowh);
   }
