@@ -69,6 +69,7 @@ int main(int argc, char** argv) {
       cn = rows * B;
     }
     const int ranges = gemm_dual_ranges(g);
+    const int E = pair == 0 && NK == NORM_CLN ? gemm_dual_group_parts(g) : 16;   // cLN entries per row
     const size_t nd = (size_t)ranges * g.Kred * g.Nout;
     std::vector<uint16_t> c0;
     std::vector<float> d0;
@@ -91,16 +92,16 @@ int main(int argc, char** argv) {
         long nbad = 0, shown = 0;
         for (long row = 0; row < rows; ++row) {
           if (row % Kp >= K) continue;
-          for (int e = 0; e < 16; ++e) {
+          for (int e = 0; e < E; ++e) {
             double hs = 0, hq = 0;
-            for (int ch = e * 32; ch < e * 32 + 32; ++ch) {
+            for (int ch = e * (H / E); ch < (e + 1) * (H / E); ++ch) {
               const float ga = bf(c[row * H + ch]);
               float x = bf(hd[row * H + ch]);
               x = x > 0.f ? x : 0.25f * x;
               hs += ga;
               hq += (double)ga * ((x - 0.1f) * 1.3f);
             }
-            const double2 v = ss[row * 16 + e];
+            const double2 v = ss[row * E + e];
             const double tol = 0.02 * (fabs(hq) + fabs(hs)) + 0.05;
             if (fabs(v.x - hs) > tol || fabs(v.y - hq) > tol) {
               ++nbad;
@@ -129,9 +130,9 @@ int main(int argc, char** argv) {
         const int ntile = (int)(rows / DU_TM), nr = ranges;
         std::vector<int> pos_from_end(8, 0), pos_from_start(8, 0);
         std::vector<int> lanegrp(4, 0), sl_nbg(16, 0);
-        for (size_t i = 0; i < (size_t)rows * 16; ++i)
+        for (size_t i = 0; i < (size_t)rows * E; ++i)
           if (memcmp(&ss[i], &s0[i], sizeof(double2))) {
-            const long row = i / 16;
+            const long row = i / E;
             const int t = (int)(row / DU_TM);
             int rr = 0;
             while ((long)ntile * (rr + 1) / nr <= t) ++rr;
@@ -139,7 +140,7 @@ int main(int argc, char** argv) {
             pos_from_end[std::min(7, t1 - 1 - t)]++;
             pos_from_start[std::min(7, t - t0)]++;
             lanegrp[(row % DU_TM) / 8]++;
-            sl_nbg[i % 16]++;
+            sl_nbg[(i % E) * (16 / E)]++;
           }
         printf("   cLN slab diffs by tile position from range end:");
         for (int v : pos_from_end) printf(" %d", v);
@@ -155,7 +156,7 @@ int main(int argc, char** argv) {
         int shown = 0;
         for (size_t i = 0; i < nslab && shown < 6; ++i)
           if (memcmp(&ss[i], &s0[i], sizeof(double2))) {
-            printf("   slab[%zu] (row %zu, entry %zu): run0 (%.9g, %.9g) now (%.9g, %.9g)\n", i, i / 16, i % 16,
+            printf("   slab[%zu] (row %zu, entry %zu): run0 (%.9g, %.9g) now (%.9g, %.9g)\n", i, i / E, i % E,
                    s0[i].x, s0[i].y, ss[i].x, ss[i].y);
             ++shown;
           }
