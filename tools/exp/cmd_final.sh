@@ -25,3 +25,5 @@ timeout -k 10 300 python bench.py --config c4 --steps 10 --warmup 3 > $O/c4.log 
 tail -1 $O/c4.log | cut -c1-200
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$O/profc4 -o run --output-format csv -- python3 bench.py --config c4 --steps 3 --warmup 1 > $O/profc4.log 2>&1 || exit 1
 python tools/prof_summary.py $(ls $O/profc4/*kernel_stats.csv | head -1) 4 12 | tee $O/c4_kernel_summary.txt
+timeout -k 10 300 python bench.py --config c5 --steps 6 --warmup 2 > $O/c5.log 2>&1 || exit 1
+tail -1 $O/c5.log | cut -c1-200
