@@ -49,7 +49,7 @@ constexpr int WS_FOLD_MAX = 512;   // utterances whose gLN operand stats a workg
 
 // Bound-finding experiments only (tools/microbench): bit 0 drops the output
 // stores, bit 1 the A-tile loads, bit 2 the MFMAs, bit 3 the epilogue math, bit 7 the
-// resident weight's loads; bit 6
+// resident weight's loads, bit 10 the dL/dh1 stores of the norm-1-backward form; bit 6
 // (experiment, not bound-finding) lets the scheduler move epilogue math into the MFMAs.
 #ifndef CTN_WS_EXP
 #define CTN_WS_EXP 0
@@ -323,7 +323,7 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
   };
   // global store of the dL/dh1 chunks staged by stage(tu)
   auto store_gh = [&](int tu) __attribute__((always_inline)) {
-    if constexpr (N1B) {
+    if constexpr (N1B && !(CTN_WS_EXP & 1024)) {   // bit 10 (timing only): no dL/dh1 stores
       if (tu < t1) {
 #pragma unroll
         for (int j = 0; j < NA; ++j) stg16(GH + (size_t)(tu * TM + rl0 + j * RSTEP) * p.lda + kc * 8, ghv[j]);
