@@ -93,6 +93,10 @@ __device__ unsigned long long ws_stamps[256 * 16 * 8];
 #endif
 // 1: wait for the resident weight before the first tiles' loads are issued; 0
 // (experiment): after them.  Measured the same.
+// cLN statistics of 64 tiles per lane, broadcast by v_readlane (see load_a)
+#ifndef CTN_WS_CLN_BATCH
+#define CTN_WS_CLN_BATCH 1
+#endif
 #ifndef CTN_WS_EARLY
 #define CTN_WS_EARLY 1
 #endif
@@ -247,6 +251,29 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
   v4u ra[PF][NA];
   float2 ast[PF][NA];
   float2 asm1[PF][N1B && NK == NORM_CLN ? NA : 1];   // N1B, cLN: per-row norm-1 backward means
+  // cLN with wave-uniform rows (a row's 16-byte chunks span whole waves): the per-row
+  // statistics (and N1B means) of 64 consecutive tiles are loaded one tile per lane and
+  // broadcast with v_readlane, instead of a load per row and tile in the prefetch
+  constexpr bool CB = CTN_WS_CLN_BATCH && NK == NORM_CLN && OPK != OP_PLAIN && !FOLDS && CPR % 64 == 0;
+  float2 bst[CB ? NA : 1], bsm[CB && N1B ? NA : 1];
+  int bbase = -(1 << 29);
+  auto batch_load = [&](int tb) __attribute__((always_inline)) {
+    if constexpr (CB) {
+      bbase = tb;
+      const int tt = tb + lane < t1 ? tb + lane : t1 - 1;
+#pragma unroll
+      for (int j = 0; j < NA; ++j) {
+        const int r = tt * TM + rl0 + j * RSTEP;
+        bst[j] = p.aop.stats[r];
+        if constexpr (N1B) bsm[j] = p.aop.sums[r];
+      }
+    }
+  };
+  auto bcast = [&](float2 v, int t) __attribute__((always_inline)) {
+    const int l = __builtin_amdgcn_readfirstlane(t - bbase);
+    return make_float2(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.x), l)),
+                       __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.y), l)));
+  };
   auto load_a = [&](int t, auto slot) __attribute__((always_inline)) {
     constexpr int s = decltype(slot)::value;
 #pragma unroll
@@ -255,8 +282,13 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
       if constexpr (CTN_WS_EXP & 2) ra[s][j] = v4u{(uint32_t)r, 0u, 0u, 0u};
       else ra[s][j] = ldg16(A + (size_t)r * p.lda + kc * 8);
       if constexpr (N1B) rh[s][j] = ldg16(H1 + (size_t)r * p.lda + kc * 8);
-      if constexpr (OPK != OP_PLAIN && !FOLDS) ast[s][j] = p.aop.stats[stat_index<NK>(r, Kp)];
-      if constexpr (N1B && NK == NORM_CLN) asm1[s][j] = p.aop.sums[r];
+      if constexpr (CB) {
+      } else if constexpr (OPK != OP_PLAIN && !FOLDS && (CTN_WS_EXP & 2048)) {
+        ast[s][j] = make_float2(0.1f, 1.3f);   // timing only: no statistics loads
+      } else if constexpr (OPK != OP_PLAIN && !FOLDS) {
+        ast[s][j] = p.aop.stats[stat_index<NK>(r, Kp)];
+      }
+      if constexpr (N1B && NK == NORM_CLN && !CB) asm1[s][j] = p.aop.sums[r];
     }
   };
   // ra -> LDS image of tile t (fragment (mb, kb) at (mb*KB + kb) KiB).  Rows of padded
@@ -269,6 +301,9 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
     constexpr int s = decltype(slot)::value;
     const int t = tu < t1 ? tu : t1 - 1;
     const int tk = (t * TM) % Kp;   // frame index of the tile's first row (wave-uniform)
+    if constexpr (CB) {
+      if (t - bbase >= 64) batch_load(t);
+    }
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
       v4u v = ra[s][j];
@@ -280,6 +315,9 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
           const int m = (t * TM) / Kp;
           sm = sst[m];
           st = sst1[m];
+        } else if constexpr (CB) {   // cLN: per-row statistics and means of this tile
+          sm = bcast(bsm[j], t);
+          st = bcast(bst[j], t);
         } else {   // cLN: per-row statistics and means, loaded with the row
           sm = asm1[s][j];
           st = ast[s][j];
@@ -303,7 +341,10 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
         }
         calpha += (tu < t1 && tk + r < Kv) ? ca : 0.f;
       } else if constexpr (OPK != OP_PLAIN) {
-        const float2 st = FOLDS ? sst[(t * TM) / Kp] : ast[s][j];
+        float2 st;
+        if constexpr (FOLDS) st = sst[(t * TM) / Kp];
+        else if constexpr (CB) st = bcast(bst[j], t);
+        else st = ast[s][j];
         float f[8];
         unpack_bf16x8(v, f);
         const f32x2_t m2 = {st.x, st.x};

@@ -58,6 +58,10 @@ int main() {
   { GemmRows g = base(H, B); g.A = d; g.C = out; g.epi = EPI_RESID; g.R = x; g.ldr = B;
     g.aop.kind = OP_PRELU_NORM; g.aop.norm = NORM_GLN; g.aop.stats = (const float2*)st; g.aop.gamma = gm; g.aop.beta = bt; g.aop.alpha = al;
     cs.push_back({"fwd2 n2.W2 + x", g, rows * (H + 2 * B) * 2.0}); }
+  {   // cLN operand (per-row statistics loaded with the rows) and cLN residual form (c4's output GEMM)
+    GemmRows g = base(H, B); g.A = d; g.C = out; g.epi = EPI_RESID; g.R = x; g.ldr = B; g.norm = NORM_CLN;
+    g.aop.kind = OP_PRELU_NORM; g.aop.norm = NORM_CLN; g.aop.stats = (const float2*)st; g.aop.gamma = gm; g.aop.beta = bt; g.aop.alpha = al;
+    cs.push_back({"fwd2 n2.W2 + x (cLN)", g, rows * (H + 2 * B) * 2.0}); }
   {   // the same with the gLN operand statistics folded from producer partials in every
       // workgroup's prologue (the library's consumer-finalized form: 144 partials per utterance)
     GemmRows g = base(H, B); g.A = d; g.C = out; g.epi = EPI_RESID; g.R = x; g.ldr = B;
