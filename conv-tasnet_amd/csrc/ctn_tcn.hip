@@ -302,20 +302,12 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
 //   gd window  gdw[i] = dL/dd   at step j + (POWN - P + 1 + i)
 //   ah window  ahw[i] = hat a1  at step j + (i - POWN)
 // ---------------------------------------------------------------------------
-// RING > 0 (bf16, gLN, H = 512: one comb item per wave): the rows of the main walk
-// arrive by LDS-DMA into a per-wave ring of RING steps (d, dL/dn2 and h1 of one step:
-// 3 KiB), RING-1 steps ahead with counted vmcnt waits, instead of register prefetch
-// (whose compiler-placed waits drained at every loop head: one row in flight per wave).
-// Each lane reads back only the 16-byte pieces it fetched itself, so a wave's own
-// vmcnt is the whole hand-off (no barrier).
-template <typename T, int NK, int P, bool CAUSAL, int RING = 0>
+template <typename T, int NK, int P, bool CAUSAL>
 __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
   constexpr int POWN = CAUSAL ? P - 1 : (P - 1) / 2;
   constexpr int GT = POWN, AT = P - 1 - POWN;           // newest step of each window, relative to j
-  static_assert(RING == 0 || (sizeof(T) == 2 && NK == NORM_GLN && RING >= 2), "ring: bf16 gLN only");
   __shared__ double red[16];
   __shared__ float buf[256 * 8];
-  __shared__ __attribute__((aligned(16))) char dring[RING > 0 ? 4 * RING * 3072 : 16];
   const CombGeom gm = comb_geom(a);
   const CombItem it = comb_item(a, gm);
   const int H = a.H, K = a.g.K, Kp = a.g.Kp, dil = a.dil, c = it.c;
@@ -526,51 +518,6 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
       }
     }
   };
-  if constexpr (RING > 0) {
-    // per-wave ring: slot s % RING holds step s (d at +0, dL/dn2 at +1 KiB, h1 at +2 KiB)
-    char* ring = dring + (threadIdx.x >> 6) * (RING * 3072);
-    const long nbytes = a.g.rows() * (long)H * 2;
-    const rsrc_t rD = du_rsrc(dd, nbytes), rG = du_rsrc(ga2, nbytes), rH = du_rsrc(h1, nbytes);
-    const uint32_t lvo = (uint32_t)lane * 16u;   // c == lane (one item per wave)
-    auto okrow = [&](int jj, bool& ok) { const int k = row_of(jj); ok = jj >= 0 && k < K; return it.base + (ok ? k : 0); };
-    auto dma = [&](int st) __attribute__((always_inline)) {
-      bool ok;
-      char* sl = ring + (st % RING) * 3072;
-      // wave-uniform rows (one item per wave): scalar offsets
-      const int og = __builtin_amdgcn_readfirstlane(okrow(st + GT, ok) * H * 2);
-      const int oh = __builtin_amdgcn_readfirstlane(okrow(st + AT, ok) * H * 2);
-      du_dma16(rD, sl, lvo, og);
-      du_dma16(rG, sl + 1024, lvo, og);
-      du_dma16(rH, sl + 2048, lvo, oh);
-    };
-    // ops issued after step j's DMA group, in the loop's fixed order [wait, reads, DMA of
-    // step i+RING-1 (while < j1), math, store of row i (while its frame < Kp)]
-    const int j0 = it.j0, j1 = it.j1;
-    const int iend = (Kp - it.rho + dil - 1) / dil;   // iterations i < iend store their row
-    auto n_st = [&](int lo, int hi) { hi = hi < iend - 1 ? hi : iend - 1; return hi >= lo ? hi - lo + 1 : 0; };
-    auto n_dma = [&](int lo, int hi) { hi = hi < j1 - RING ? hi : j1 - RING; return hi >= lo ? hi - lo + 1 : 0; };
-    auto ops_after = [&](int j) __attribute__((always_inline)) {
-      if (j <= j0 + RING - 2) {   // issued by the prologue
-        const int plast = j0 + RING - 2 < j1 - 1 ? j0 + RING - 2 : j1 - 1;
-        return 3 * (plast - j) + 3 * n_dma(j0, j - 1) + n_st(j0, j - 1);
-      }
-      const int ii = j - RING + 1;   // the iteration that issued it
-      return n_st(ii, ii) + 3 * n_dma(ii + 1, j - 1) + n_st(ii + 1, j - 1);
-    };
-    for (int st = j0; st < j1 && st <= j0 + RING - 2; ++st) dma(st);
-    for (int j = j0; j < j1; ++j) {
-      vmwait23(__builtin_amdgcn_readfirstlane(ops_after(j)));
-      const char* sl = ring + (j % RING) * 3072 + lane * 16;
-      Raw8<T> cd, cgv, ch;
-      cd.v = *reinterpret_cast<const u128*>(sl);
-      cgv.v = *reinterpret_cast<const u128*>(sl + 1024);
-      ch.v = *reinterpret_cast<const u128*>(sl + 2048);
-      if (j + RING - 1 < j1) dma(j + RING - 1);
-      bool cok, cokh;
-      const int crow = okrow(j + GT, cok), crowh = okrow(j + AT, cokh);
-      body(j, cd, cgv, ch, cok, cokh, crow, crowh);
-    }
-  } else {
   Raw8<T> pd[D], pg[D], ph[D]; bool pok[D], pokh[D]; int prow[D], prowh[D];
 #pragma unroll
   for (int q = 0; q < D; ++q) {
@@ -596,7 +543,6 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
       }
     }
     body(j, cd, cgv, ch, cok, cokh, crow, crowh);
-  }
   }
   if constexpr (NK != NORM_GLN)
     if (wave_item && it.j1 > pk.j0) park_flush(it.j1 - pk.j0);
@@ -735,25 +681,10 @@ static hipError_t dw_check(const DwArgs& a) {
 
 CTN_DW_P_KERNEL(dw_fwd)
 
-// dw_bwd: CTN_DW_RING > 0 builds the LDS-DMA ring variant (bf16, gLN, H = 512) with
-// that depth.  Experiment, off: 100.5 against 91 us in the step -- the
-// kernel is bound by its ~350 instructions per row at two waves per SIMD, not by rows
-// in flight.
-#ifndef CTN_DW_RING
-#define CTN_DW_RING 0
-#endif
 template <typename T, int NK, int P>
 static void dw_bwd_launch(const DwArgs& a, hipStream_t s) {
   const bool causal = a.pad / a.dil == P - 1 && P > 1 && (P - 1) != (P - 1) / 2;
   const dim3 grid(dw_blocks(a)), blk(256);
-  if constexpr (CTN_DW_RING > 0 && sizeof(T) == 2 && NK == NORM_GLN) {
-    static const bool ring = [] { const char* e = getenv("CTN_DW_RING"); return !e || atoi(e) != 0; }();
-    if (ring && a.H == 512) {
-      if (causal) hipLaunchKernelGGL((dw_bwd_kernel<T, NK, P, true, CTN_DW_RING>), grid, blk, 0, s, a);
-      else hipLaunchKernelGGL((dw_bwd_kernel<T, NK, P, false, CTN_DW_RING>), grid, blk, 0, s, a);
-      return;
-    }
-  }
   if (causal) hipLaunchKernelGGL((dw_bwd_kernel<T, NK, P, true>), grid, blk, 0, s, a);
   else hipLaunchKernelGGL((dw_bwd_kernel<T, NK, P, false>), grid, blk, 0, s, a);
 }
