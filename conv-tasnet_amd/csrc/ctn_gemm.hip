@@ -706,10 +706,21 @@ __global__ __launch_bounds__(CTHREADS) void gemm_cols_kernel(GemmCols p) {
     }
 }
 
+// target workgroup count of a column GEMM (CTN_COLS_WG overrides it for A/B experiments)
+static int cols_wg_target() {
+  static int t = 0;
+  if (!t) {
+    const char* e = getenv("CTN_COLS_WG");
+    const int v = e ? atoi(e) : 0;
+    t = v >= 64 && v <= 4096 ? v : 256;
+  }
+  return t;
+}
+
 int gemm_cols_default_chunks(const GemmCols& p) {
   const int tiles = ((p.P + CBP - 1) / CBP) * ((p.Q + CBQ - 1) / CBQ);
   const long rows = p.g.rows();
-  int ch = (256 + tiles - 1) / tiles;            // ~256 workgroups of CKS x 4 waves
+  int ch = (cols_wg_target() + tiles - 1) / tiles;   // ~256 workgroups of CKS x 4 waves
   const long maxch = (rows + CKS * CKR * 4 - 1) / (CKS * CKR * 4);   // >= 4 k-steps per group
   if (ch > maxch) ch = (int)maxch;
   return ch < 1 ? 1 : ch;

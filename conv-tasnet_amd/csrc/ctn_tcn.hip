@@ -833,22 +833,31 @@ struct SrJob {
   int nparts, n, pstride, nslices;
   int vec4;   // 4 consecutive outputs per lane (16-byte loads); same per-output order
 };
+// The grid is flat: job jb owns workgroups [wg0[jb], wg0[jb+1]), one per (slice, output
+// tile) pair, so no workgroup is launched only to exit (a (tiles, slices, jobs) grid sized
+// by the largest job launched ~70k workgroups per block backward for ~1.3k with work).
 struct SrBatch {
   SrJob j[16];
+  int wg0[17];   // prefix sums of the jobs' workgroup counts
+  int ntx[16];   // output tiles per slice
   int nj;
 };
 
 __global__ __launch_bounds__(256) void slab_reduce_kernel(SrBatch b) {
   __shared__ double part[4][64];
   __shared__ double part4[4][4][64];
-  const SrJob d = b.j[blockIdx.z];
-  if ((int)blockIdx.y >= d.nslices) return;
+  int jb = 0;
+  while (jb + 1 < b.nj && (int)blockIdx.x >= b.wg0[jb + 1]) ++jb;
+  const SrJob d = b.j[jb];
+  const int ntx = b.ntx[jb];
+  const int loc = (int)blockIdx.x - b.wg0[jb];
+  const int sl = loc / ntx, tx = loc - sl * ntx;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int q0 = blockIdx.y * SR_SLICE;
+  const int q0 = sl * SR_SLICE;
   const int q1 = d.nslices == 1 ? d.nparts : (q0 + SR_SLICE < d.nparts ? q0 + SR_SLICE : d.nparts);
-  float* out = d.nslices > 1 ? d.dst + (size_t)blockIdx.y * d.n : d.dst;
+  float* out = d.nslices > 1 ? d.dst + (size_t)sl * d.n : d.dst;
   if (d.vec4) {   // lanes own 4 consecutive outputs: 1 KiB per wave load instead of 256 B
-    for (int i0 = blockIdx.x * 256; i0 < d.n; i0 += gridDim.x * 256) {
+    for (int i0 = tx * 256; i0 < d.n; i0 += ntx * 256) {
       const int i = i0 + 4 * lane;
       double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
       if (i < d.n) {
@@ -891,7 +900,7 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(SrBatch b) {
     }
     return;
   }
-  for (int i0 = blockIdx.x * 64; i0 < d.n; i0 += gridDim.x * 64) {
+  for (int i0 = tx * 64; i0 < d.n; i0 += ntx * 64) {
     const int i = i0 + lane;
     double acc = 0.0;
     if (i < d.n) {
@@ -913,17 +922,20 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(SrBatch b) {
   }
 }
 
-static hipError_t sr_launch(const SrBatch& b, hipStream_t s) {
+static hipError_t sr_launch(SrBatch b, hipStream_t s) {
   if (b.nj <= 0) return hipSuccess;
-  int gx = 1, ms = 1;
+  long tot = 0;
   for (int i = 0; i < b.nj; ++i) {
     const int per = b.j[i].vec4 ? 256 : 64;
-    const int g = (b.j[i].n + per - 1) / per;
-    gx = g > gx ? g : gx;
-    ms = b.j[i].nslices > ms ? b.j[i].nslices : ms;
+    int g = (b.j[i].n + per - 1) / per;
+    if (g > 1024) g = 1024;   // larger outputs: grid-stride over the tiles
+    if (g < 1) g = 1;
+    b.ntx[i] = g;
+    b.wg0[i] = (int)tot;
+    tot += (long)g * b.j[i].nslices;
   }
-  if (gx > 1024) gx = 1024;
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3(gx, ms, b.nj), dim3(256), 0, s, b);
+  b.wg0[b.nj] = (int)tot;
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)tot), dim3(256), 0, s, b);
   return hipGetLastError();
 }
 
