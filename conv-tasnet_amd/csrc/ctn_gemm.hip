@@ -439,14 +439,18 @@ template <> CTN_DEV int cswz<float>(int row, int col) { return row * ColsPitch<f
 // own LDS stages, and add their 128x128 accumulators through LDS at the end: one
 // partial per chunk from 8 waves halves the partial-sum traffic (write here, read
 // by the slab reduction) of 4-wave workgroups at the same occupancy.
-constexpr int CKS = 2;                           // k-split groups per workgroup
-constexpr int CTHREADS = 256 * CKS;
+#ifndef CTN_COLS_CKS
+#define CTN_COLS_CKS 2   // bf16 k-split groups per workgroup (experiment switch)
+#endif
+template <typename T> struct ColsCks { static constexpr int v = sizeof(T) == 2 ? CTN_COLS_CKS : 2; };
+constexpr int CKS = 2;                           // k-split groups per workgroup (host-side sizing)
 
 template <typename T, int OPA, int OPB, int NK>
-__global__ __launch_bounds__(CTHREADS) void gemm_cols_kernel(GemmCols p) {
+__global__ __launch_bounds__(256 * ColsCks<T>::v) void gemm_cols_kernel(GemmCols p) {
+  constexpr int CKS = ColsCks<T>::v;
   constexpr int PITCH = ColsPitch<T>::v;
   constexpr int STAGE = 2 * CKR * PITCH;         // one k-step: A tile then B tile
-  static_assert(CKS * 2 * STAGE >= (CKS - 1) * CBP * CBQ * 4, "accumulator exchange fits the stages");
+  static_assert(CKS * 2 * STAGE >= CBP * CBQ * 4, "accumulator exchange (one group at a time) fits the stages");
   __shared__ __attribute__((aligned(16))) char smem_all[CKS * 2 * STAGE];
   constexpr int E = Chunk<T>::E;
   constexpr int CPR = CBP * sizeof(T) / 16;      // 16-byte chunks per LDS row
@@ -729,7 +733,7 @@ int gemm_cols_default_chunks(const GemmCols& p) {
 template <typename T, int OPA, int OPB, int NK>
 static hipError_t launch_cols_t(const GemmCols& p, hipStream_t s) {
   const int tiles = ((p.P + CBP - 1) / CBP) * ((p.Q + CBQ - 1) / CBQ);
-  hipLaunchKernelGGL((gemm_cols_kernel<T, OPA, OPB, NK>), dim3(tiles * p.nchunks), dim3(CTHREADS), 0, s, p);
+  hipLaunchKernelGGL((gemm_cols_kernel<T, OPA, OPB, NK>), dim3(tiles * p.nchunks), dim3(256 * ColsCks<T>::v), 0, s, p);
   return hipGetLastError();
 }
 
