@@ -8,7 +8,12 @@ HDR      := $(wildcard $(PKG)/csrc/*.h) include/ctn.h
 # device codegen: MFMA accumulators in VGPRs (no accvgpr copies around the MFMAs;
 # gemm_cols 83 -> 55 us).  IEEE mode stays on: turning it off measured neutral
 # everywhere except the NORM_BWD WS GEMM, which it slowed by 9%.
-DEVFLAGS := -mllvm -amdgpu-mfma-vgpr-form
+# Packed FP32 (v_pk_fma/mul/add_f32) is off: on gfx950 a packed instruction that takes a
+# source half through op_sel/op_sel_hi (the compiler's splat of a scalar operand) right
+# after the VALU instruction that wrote that register occasionally reads the old value
+# when another wave on the SIMD is busy; the compiler inserts no wait state for it
+# (tools/microbench/pk_hazard.hip).
+DEVFLAGS := -mllvm -amdgpu-mfma-vgpr-form -Xclang -target-feature -Xclang -packed-fp32-ops
 CXXFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function -Iinclude $(DEVFLAGS)
 LIB      := $(PKG)/libctn_hip.so
 
@@ -43,3 +48,21 @@ build/dual_bench_%: tools/microbench/dual_bench.hip $(PKG)/csrc/ctn_gemm_dual.hi
 	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -Iinclude $(DEVFLAGS) -DCTN_DU_EXP=$* $< -o $@
 
 .PHONY: dualbench
+
+# wave-specialised pair-A dual GEMM vs gemm_dual_kernel: build/dual_ws_bench_<bits>
+DV_EXPS := 0 1 2 4 6
+dualws: $(patsubst %,build/dual_ws_bench_%,$(DV_EXPS))
+build/dual_ws_bench_%: tools/microbench/dual_ws_bench.hip $(PKG)/csrc/ctn_dual_ws.hip $(PKG)/csrc/ctn_gemm_dual.hip $(HDR)
+	@mkdir -p build
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -Iinclude $(DEVFLAGS) -DCTN_DV_EXP=$* $< -o $@
+
+.PHONY: dualws
+
+# diagnostic builds of the wave-specialised kernel: build/dual_ws_dbg_<bits>
+DV_DBGS := 16 17 18 20 0 8
+dualwsdbg: $(patsubst %,build/dual_ws_dbg_%,$(DV_DBGS))
+build/dual_ws_dbg_%: tools/microbench/dual_ws_bench.hip $(PKG)/csrc/ctn_dual_ws.hip $(PKG)/csrc/ctn_gemm_dual.hip $(HDR)
+	@mkdir -p build
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -Iinclude $(DEVFLAGS) -DCTN_DV_DBG=$* $< -o $@
+
+.PHONY: dualwsdbg

@@ -184,15 +184,53 @@ def spawn_ranks(n, cmd, port=None, env=None):
     for r in range(n):
         e = dict(base, RANK=str(r), LOCAL_RANK=str(r))
         procs.append(subprocess.Popen(cmd, env=e))
+    # Poll every rank: a rank that dies while another is blocked inside a collective
+    # (which would only return at the RCCL timeout) must still end the job at once.
     rc = 0
-    for p in procs:
-        code = p.wait()
-        if code and not rc:
-            rc = code
-            for q in procs:              # one rank failed: the others would wait forever
-                if q.poll() is None:
-                    q.terminate()
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                break
+            if all(c == 0 for c in codes):
+                break
+            time.sleep(0.05)
+    finally:
+        for q in procs:                  # one rank failed: the others would wait forever
+            if q.poll() is None:
+                q.terminate()
+        for q in procs:
+            try:
+                q.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                q.kill()
+                q.wait()
     return rc
+
+
+def visible_gpus():
+    """GPUs this process may use, without initialising HIP in this process: the
+    *_VISIBLE_DEVICES lists if set, else the GPU nodes of the KFD topology (sysfs)."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return len([x for x in v.split(",") if x.strip() not in ("", "-1")])
+    nodes = "/sys/class/kfd/kfd/topology/nodes"
+    n = 0
+    try:
+        for d in os.listdir(nodes):
+            try:
+                with open(os.path.join(nodes, d, "properties")) as f:
+                    props = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
+            except OSError:
+                continue
+            if int(props.get("simd_count", "0")) > 0:    # CPU nodes have no SIMDs
+                n += 1
+    except OSError:
+        return 0
+    return n
 
 
 def main():
@@ -212,9 +250,9 @@ def main():
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        # no outside launcher: start one rank per GPU ourselves (children, no exec);
-        # counting devices does not initialise the GPU in this (parent) process
-        visible = torch.cuda.device_count()
+        # no outside launcher: start one rank per GPU ourselves (children, no exec); the
+        # GPUs are counted from the environment / sysfs, so this parent never loads HIP
+        visible = visible_gpus()
         if args.gpus > visible:
             sys.exit(f"bench.py: --gpus {args.gpus} but only {visible} GPU(s) visible")
         sys.exit(spawn_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
@@ -293,10 +331,14 @@ def main():
     nl = ctypes.c_int(0)
     L.check(lib.ctn_timer_read(ctypes.byref(tot), ctypes.byref(nl)), "ctn_timer_read")
     lib.ctn_timer_enable(0, 0)
+    rank_ms = [round(elapsed / args.steps * 1e3, 3)]
     if use_ddp:
+        # every rank's time (max = the job's time); the list's length is RCCL's world size
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t)
+        ts = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+        dist.all_gather(ts, t)
+        rank_ms = [round(float(x) / args.steps * 1e3, 3) for x in ts]
+        elapsed = max(float(x) for x in ts)
     final_loss = float(loss)
 
     if rank == 0:
@@ -341,7 +383,9 @@ def main():
                                     f"{'causal' if cfg['causal'] else 'non-causal'} relu-mask, {C} spk, "
                                     f"{args.seconds:g} s @ {rate // 1000} kHz, fwd+PIT loss+bwd+clip+Adam"),
                        "per_gpu_batch": M, "global_batch": M * world, "samples": T, "frames": K,
-                       "parallelism": f"dp{world}" + (" (DDP/RCCL)" if use_ddp else "")},
+                       "parallelism": f"dp{world}" + (" (DDP/RCCL)" if use_ddp else ""),
+                       "rccl_world_size": dist.get_world_size() if use_ddp else None,
+                       "rank_ms_per_step": rank_ms},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": {1: "gemm_ws fwd 1x1 B->H (PReLU-stats epilogue)",

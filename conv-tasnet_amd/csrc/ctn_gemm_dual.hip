@@ -610,6 +610,7 @@ bool gemm_dual_eligible(DType dt, const GemmDual& p) {
   const bool pairB = p.Kred == 512 && p.epi == EPI_RESID && p.bop.kind == OP_PLAIN;
   const int mask = dual_mask();
   if (!(pairA && (mask & 1)) && !(pairB && (mask & 2))) return false;
+  if (pairA && gemm_dual_ws_eligible(p)) return true;            // wave-specialised kernel (ctn_dual_ws.hip)
   if (p.bop.kind != OP_PLAIN && p.bop.fold.slab) return false;   // needs final statistics
   if (p.g.Kp % DU_TM || p.lda % 8 || p.ldw % 8 || p.ldc % 8 || p.ldr % 8 || p.ldb % 8) return false;
   if (p.g.rows() / DU_TM < 1 || p.g.rows() * (p.Kred > p.Nout ? p.Kred : p.Nout) * 2 >= (1L << 31)) return false;
@@ -643,7 +644,7 @@ WsRuns gemm_dual_runs(const GemmDual& p) {
 int gemm_dual_group_parts(const GemmDual& p) {
   int kb, nsb, nbw;
   dual_shape(p.Kred, p.Nout, &kb, &nsb, &nbw);
-  if (p.norm != NORM_GLN) return dual_slices(p) * (nsb / nbw);
+  if (p.norm != NORM_GLN) return gemm_dual_ws_eligible(p) ? dual_slices(p) : dual_slices(p) * (nsb / nbw);
   const WsRuns w = gemm_dual_runs(p);
   const long entries = (long)w.grid * w.waves * w.kmax;
   return (int)((entries + p.g.M - 1) / p.g.M);
@@ -677,6 +678,7 @@ static hipError_t dual_launch_nk(const GemmDual& p, hipStream_t s) {
 
 hipError_t launch_gemm_dual(const GemmDual& p, hipStream_t s) {
   if (!gemm_dual_eligible(BF16, p)) return hipErrorInvalidValue;
+  if (gemm_dual_ws_eligible(p)) return launch_gemm_dual_ws(p, s);
   const int nk = p.bop.kind != OP_PLAIN ? p.bop.norm : p.norm;
   return nk == NORM_GLN ? dual_launch_nk<NORM_GLN>(p, s) : dual_launch_nk<NORM_CLN>(p, s);
 }

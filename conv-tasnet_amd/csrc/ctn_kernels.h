@@ -119,6 +119,11 @@ int gemm_dual_group_parts(const GemmDual& p);
 StatFold gemm_dual_stat_fold(const GemmDual& p, const double2* slab, double cnt, float eps, int mode,
                              float2* out);
 hipError_t launch_gemm_dual(const GemmDual& p, hipStream_t s);
+// wave-specialised pair-A kernel (ctn_dual_ws.hip), chosen by launch_gemm_dual
+bool gemm_dual_ws_enabled();
+bool gemm_dual_ws_eligible(const GemmDual& p);
+int gemm_dual_ws_ranges(const GemmDual& p);
+hipError_t launch_gemm_dual_ws(const GemmDual& p, hipStream_t s);
 
 // ---- statistics ------------------------------------------------------------
 // slab: [G][nparts] double2 partials -> out[G] float2

@@ -139,6 +139,9 @@ def bn_state(bn1: torch.nn.BatchNorm1d, bn2: torch.nn.BatchNorm1d) -> tuple:
 # parameter gradients on a second stream (ctn_tblock_backward_split)
 # ----------------------------------------------------------------------------
 _WGRAD_STREAMS = {}
+# (device, autograd graph task) pairs whose end-of-backward join is queued.  Keyed by the
+# graph task, not just the device: a backward that raises after queueing drops its
+# callbacks, and a stale device-only entry would stop every later backward from joining.
 _WGRAD_PENDING = set()
 
 
@@ -149,10 +152,10 @@ def _wgrad_stream(device) -> torch.cuda.Stream:
     return st
 
 
-def _join_wgrad(device):
+def _join_wgrad(device, key):
     """End of the backward pass: the caller's stream waits for the parameter-gradient
     stream, so every consumer of .grad (clip, optimizer, user code) sees them done."""
-    _WGRAD_PENDING.discard(device)
+    _WGRAD_PENDING.discard(key)
     torch.cuda.current_stream(device).wait_stream(_wgrad_stream(device))
 
 
@@ -252,10 +255,11 @@ class TBlockFn(torch.autograd.Function):
             t.record_stream(side)
         for p, g in zip(ctx.param_refs, grads):
             p.grad = g
-        if x.device not in _WGRAD_PENDING:
-            _WGRAD_PENDING.add(x.device)
+        key = (x.device, torch._C._current_graph_task_id())
+        if key not in _WGRAD_PENDING:
+            _WGRAD_PENDING.add(key)
             dev = x.device
-            torch.autograd.Variable._execution_engine.queue_callback(lambda: _join_wgrad(dev))
+            torch.autograd.Variable._execution_engine.queue_callback(lambda: _join_wgrad(dev, key))
         return (gx, None, None, None, None) + (None,) * 9
 
 

@@ -58,6 +58,8 @@ class StreamingSeparator:
     """
 
     def __init__(self, model: ConvTasNet, act_dtype=None, max_frames: int = 64):
+        """act_dtype: None or torch.float32 — the stream kernels compute and keep their
+        state in fp32 (the round-2 bf16 streamer was replaced; bf16 raises ValueError)."""
         if not model.causal:
             raise ValueError("streaming needs a causal model (ConvTasNet(causal=True))")
         norm = _norm_code(model.norm_type)
@@ -178,9 +180,10 @@ class StreamingSeparator:
 
     @torch.no_grad()
     def flush(self) -> torch.Tensor:
-        """The remaining overlap-add samples (call once after the last chunk)."""
+        """The remaining overlap-add samples (call once after the last chunk).  The
+        streamer is reset afterwards: the next push() starts a new stream."""
         out = self.tail if self.frames else None
-        self.tail = None
+        self.reset()
         if out is None:
             return torch.zeros(0)
         return out

@@ -48,3 +48,32 @@ def test_bench_refuses_more_gpus_than_visible():
                        env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode != 0
     assert "GPU(s) visible" in p.stderr
+
+
+def test_spawn_ranks_ends_the_job_when_a_later_rank_dies():
+    """Rank 1 exits with 3 while rank 0 blocks in a gloo barrier that can never
+    complete: the launcher must return 3 promptly (it polls every rank), not wait
+    for rank 0's collective timeout."""
+    import time
+    stub = (
+        "import os, sys, datetime, torch.distributed as dist\n"
+        "dist.init_process_group('gloo', timeout=datetime.timedelta(seconds=600))\n"
+        "if os.environ['RANK'] == '1':\n"
+        "    os._exit(3)\n"
+        "dist.barrier()\n"
+    )
+    t0 = time.time()
+    rc = bench.spawn_ranks(2, [sys.executable, "-c", stub])
+    assert rc == 3
+    assert time.time() - t0 < 120
+
+
+def test_visible_gpus_counts_without_hip(monkeypatch):
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1,2")
+    assert bench.visible_gpus() == 3
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
+    assert bench.visible_gpus() == 0
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES")
+    monkeypatch.delenv("ROCR_VISIBLE_DEVICES", raising=False)
+    monkeypatch.delenv("CUDA_VISIBLE_DEVICES", raising=False)
+    assert bench.visible_gpus() >= 0      # sysfs count (0 in a container without a GPU)

@@ -116,3 +116,17 @@ def test_stream_rejects_non_streamable_models():
     m = ct.ConvTasNet(16, 16, 8, 16, 3, 2, 1, 2, norm_type="BN", causal=True).to(DEV)
     with pytest.raises(ValueError):
         streaming.StreamingSeparator(m.train())
+
+
+def test_stream_push_after_flush_starts_a_new_stream():
+    """flush() leaves the streamer reset: pushing the same signal again reproduces the
+    first stream exactly (no stale rings, tail or pending samples)."""
+    import streaming
+    m = _model()
+    mix = torch.randn(2, 2000, device=DEV)
+    s = streaming.StreamingSeparator(m)
+    first = torch.cat([s.push(mix[:, :700]), s.push(mix[:, 700:]), s.flush()], dim=2)
+    second = torch.cat([s.push(mix[:, :700]), s.push(mix[:, 700:]), s.flush()], dim=2)
+    assert torch.equal(first, second)
+    with pytest.raises(ValueError):
+        streaming.StreamingSeparator(m, act_dtype=torch.bfloat16)

@@ -84,3 +84,46 @@ def test_split_not_used_when_observable():
     h.remove()
     idx = [i for i, p in enumerate(params) if p is w][0]
     assert len(seen) == 1 and torch.equal(seen[0], ref[idx])
+
+
+def test_split_join_survives_a_failed_backward(monkeypatch):
+    """A backward that raises after split blocks queued their end-of-backward join
+    drops the callback; the next split backward must still queue (and run) its own
+    join, so .grad is never read while the side stream may still write it."""
+    import ctn_ops as ops
+    import pit_criterion as pc
+    m = _model()
+    torch.manual_seed(3)
+    mix = torch.randn(2, 4000, device=DEV)
+    src = torch.randn(2, 2, 4000, device=DEV)
+    lens = torch.full((2,), 4000, device=DEV)
+    ref = _grads(m, mix, src, False)
+
+    joins = []
+    real_join = ops._join_wgrad
+    monkeypatch.setattr(ops, "_join_wgrad", lambda *a: (joins.append(a), real_join(*a)))
+
+    def boom(_):
+        raise RuntimeError("injected failure after the blocks' backward")
+
+    m.wgrad_stream = True
+    m.zero_grad(set_to_none=True)
+    # the hook on the first block's input fires after every block's backward has run
+    blk0 = next(m.separator.blocks())
+    fwd = blk0._forward_rows
+
+    def hooked(x, *a):
+        x.register_hook(boom)
+        return fwd(x, *a)
+
+    monkeypatch.setattr(blk0, "_forward_rows", hooked)
+    with pytest.raises(RuntimeError, match="injected failure"):
+        pc.cal_loss(src, m(mix), lens)[0].backward()
+    monkeypatch.setattr(blk0, "_forward_rows", fwd)
+    torch.cuda.synchronize()
+    n0 = len(joins)                         # the engine drops a failed pass's callbacks
+
+    got = _grads(m, mix, src, True)
+    assert len(joins) == n0 + 1             # the next pass joins anyway
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b)
