@@ -1641,3 +1641,65 @@ extern "C" int ctn_stream_decode(const ctn_stream_desc* d, const float* x_last, 
   CTN_HIP(launch_stream(3, a, (hipStream_t)stream));
   return CTN_OK;
 }
+
+// ABI v7: one whole streaming call (ctn_stream.hip, launch_stream_call_stage)
+extern "C" size_t ctn_stream_workspace_bytes(const ctn_stream_desc* d) {
+  if (stream_check(d)) return 0;
+  const size_t M = d->M, K = d->K;
+  const size_t f = M * K * d->N + 2 * M * K * d->B + M * K * (size_t)(d->H > d->C * d->N ? d->H : d->C * d->N);
+  return f * sizeof(float) + 256;
+}
+
+extern "C" int ctn_stream_call(const ctn_stream_desc* d, const ctn_stream_model* mdl, int64_t pos, const float* samples,
+                               int64_t ld_samples, const float* tail_in, float* tail_out, float* out, void* ws,
+                               size_t ws_bytes, void* stream) {
+  if (int rc = stream_check(d)) return rc;
+  if (!mdl || !samples || !tail_in || !tail_out || !out || !ws) return fail(CTN_ERR_ARG, "null pointer");
+  if (!mdl->U || !mdl->gamma0 || !mdl->beta0 || !mdl->wb_t || !mdl->wm_t || !mdl->V || (mdl->nblocks && !mdl->blocks))
+    return fail(CTN_ERR_ARG, "null model pointer");
+  if (mdl->nblocks < 0) return fail(CTN_ERR_ARG, "nblocks %d", mdl->nblocks);
+  if (pos < 0) return fail(CTN_ERR_ARG, "pos %lld", (long long)pos);
+  if (tail_in == tail_out) return fail(CTN_ERR_ARG, "tail_out must not alias tail_in");
+  if (ld_samples < (int64_t)(d->K - 1) * (d->L / 2) + d->L) return fail(CTN_ERR_ARG, "ld_samples too small");
+  if (ws_bytes < ctn_stream_workspace_bytes(d)) return fail(CTN_ERR_ARG, "workspace too small");
+  for (int i = 0; i < mdl->nblocks; ++i) {
+    const ctn_stream_block_params& b = mdl->blocks[i];
+    if (b.dilation < 1 || b.ring_frames < 1 || (b.ring_frames & (b.ring_frames - 1)) ||
+        b.ring_frames < (d->P - 1) * b.dilation + d->K)
+      return fail(CTN_ERR_ARG, "block %d: dilation %d, ring_frames %d (a power of two >= (P-1)*dilation + K)", i,
+                  b.dilation, b.ring_frames);
+    if (!b.w1_t || !b.alpha1 || !b.norm1_a || !b.norm1_b || !b.wd || !b.alpha2 || !b.norm2_a || !b.norm2_b ||
+        !b.w2_t || !b.ring)
+      return fail(CTN_ERR_ARG, "block %d: null pointer", i);
+  }
+  const hipStream_t s = (hipStream_t)stream;
+  const size_t M = d->M, K = d->K;
+  float* w = reinterpret_cast<float*>(ws);
+  float* xa = w + M * K * d->N;
+  float* xb = xa + M * K * d->B;
+  float* scratch = xb + M * K * d->B;   // h1 of a block / the sources
+  StreamArgs a = stream_args(d);
+  a.pos = pos;
+  a.samples = samples; a.ld_samples = ld_samples; a.U = mdl->U; a.na = mdl->gamma0; a.nb = mdl->beta0;
+  a.W = mdl->wb_t; a.w_out = w; a.x_out = xa;
+  CTN_HIP(launch_stream_call_stage(0, a, s));
+  float* x = xa;
+  float* y = xb;
+  for (int i = 0; i < mdl->nblocks; ++i) {
+    const ctn_stream_block_params& b = mdl->blocks[i];
+    StreamArgs ab = stream_args(d);
+    ab.pos = pos; ab.dil = b.dilation; ab.R = b.ring_frames; ab.ring = b.ring;
+    ab.x_in = x; ab.x_out = y; ab.frames = scratch;
+    ab.W = b.w1_t; ab.alpha1 = b.alpha1; ab.na = b.norm1_a; ab.nb = b.norm1_b;
+    ab.wd = b.wd; ab.alpha2 = b.alpha2; ab.na2 = b.norm2_a; ab.nb2 = b.norm2_b; ab.W2 = b.w2_t;
+    CTN_HIP(launch_stream_call_stage(1, ab, s));
+    CTN_HIP(launch_stream_call_stage(2, ab, s));
+    float* t = x; x = y; y = t;
+  }
+  StreamArgs ad = stream_args(d);
+  ad.x_in = x; ad.w_in = w; ad.W = mdl->wm_t; ad.V = mdl->V; ad.frames = scratch;
+  ad.tail_in = tail_in; ad.tail_out = tail_out; ad.out = out;
+  CTN_HIP(launch_stream_call_stage(3, ad, s));
+  CTN_HIP(launch_stream_call_stage(4, ad, s));
+  return CTN_OK;
+}

@@ -121,6 +121,7 @@ CTN_DEV void du_dma4(rsrc_t r, const char* lds, uint32_t voff, int soff) {
                : "v"(voff), "s"(r), "s"(du_ldsaddr(lds)), "s"(soff)
                : "memory");
 }
+constexpr uint32_t DU_OOB = 0x80000000u;   // voffset past every buffer: loads (and LDS-DMA) return 0
 // s_waitcnt vmcnt(n) for a wave-uniform n (clamped down: waiting for more is safe)
 CTN_DEV void du_vmwait(int n) {
   switch (n < 0 ? 0 : n) {

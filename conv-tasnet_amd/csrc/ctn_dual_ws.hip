@@ -40,11 +40,13 @@ typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 constexpr int DV_TM = 32;                        // frame rows per tile
-constexpr int DV_NC = 8, DV_NMW = 4;             // consumer / memory waves
-constexpr int DV_NT = (DV_NC + DV_NMW) * 64;     // 768 threads
+constexpr int DV_NR = 4, DV_NC = 8, DV_NMW = 4;  // row / column / memory waves
+constexpr int DV_ND = DV_NR + DV_NC;             // waves that publish DONE
+constexpr int DV_NT = (DV_ND + DV_NMW) * 64;     // 1024 threads
 constexpr int DV_KB = 8, DV_KR = 256;            // reduction of the row part (gy channels)
 constexpr int DV_NS = 128;                       // output channels per slice
 constexpr int DV_GRID = 256;
+constexpr int DV_NSL = 4;                        // LDS ring slots (NSL - 1 tiles in flight)
 
 // Bound-finding builds only (tools/microbench/dual_bench.hip -DCTN_DV_EXP=<bits>):
 // bit 0 consumers skip all arithmetic (wait FULL, publish DONE), bit 1 no column part,
@@ -65,12 +67,9 @@ constexpr int DV_A = DV_TM * DV_KR * 2;          // 16384: gy tile, WS fragment 
 constexpr int DV_BST = 1024 + 32;                // B image block stride: 16 columns x 32 rows + 32 B
 constexpr int DV_B = 8 * DV_BST;                 // op(d) slice in 4-row x 16-column blocks (du_boff)
 constexpr int DV_R = DV_TM * DV_NS * 2;          // 8192: raw d rows, 16-byte granules XOR row
-constexpr int DV_C = DV_R;                       // C image, same addressing as R
-constexpr int DV_ST = DV_TM * 8;                 // (mean, rstd): per row (cLN) or the tile's utterance (gLN)
-constexpr int DV_PT = DV_TM * DV_NC * 8;         // cLN: per-row (sum ga, sum ga*hat a) of each consumer
-constexpr int OFF_A = 0, OFF_B = OFF_A + DV_A, OFF_R = OFF_B + DV_B, OFF_C = OFF_R + DV_R;
-constexpr int OFF_ST = OFF_C + DV_C, OFF_PT = OFF_ST + DV_ST;
-template <int NK> constexpr int dv_slot() { return NK == NORM_CLN ? OFF_PT + DV_PT : OFF_ST + 16; }
+constexpr int DV_ST = DV_NMW * 256;              // statistics: 256 B per memory wave
+constexpr int OFF_A = 0, OFF_B = OFF_A + DV_A, OFF_R = OFF_B + DV_B, OFF_ST = OFF_R + DV_R;
+constexpr int DV_SLOT = OFF_ST + DV_ST;
 
 // 16-byte piece kc (8 channels) of frame row `row` in the A image (as ctn_gemm_dual.hip's du_apiece)
 CTN_DEV int dv_apiece(int row, int kc) {
@@ -101,14 +100,14 @@ CTN_DEV s16x4_t dv_tr(const char* p) {
 typedef __attribute__((address_space(3))) volatile v4u lds_v4u;
 typedef __attribute__((address_space(3))) volatile uint32_t lds_u32;
 template <int N> CTN_DEV void dv_wait(const uint32_t* f, uint32_t gen) {
-  static_assert(N == 4 || N == 8, "generation words per slot");
+  static_assert(N % 4 == 0, "generation words per slot: whole 16-byte reads");
   const lds_v4u* fl = (const lds_v4u*)(f);
   for (uint32_t it = 0; it < (1u << 22); ++it) {
-    const v4u a = fl[0];
-    uint32_t mn = min(min(a[0], a[1]), min(a[2], a[3]));
-    if constexpr (N == 8) {
-      const v4u b = fl[1];
-      mn = min(mn, min(min(b[0], b[1]), min(b[2], b[3])));
+    uint32_t mn = 0xffffffffu;
+#pragma unroll
+    for (int i = 0; i < N / 4; ++i) {
+      const v4u a = fl[i];
+      mn = min(mn, min(min(a[0], a[1]), min(a[2], a[3])));
     }
     if (__builtin_amdgcn_readfirstlane(mn) >= gen) break;
     __builtin_amdgcn_s_sleep(1);
@@ -125,11 +124,11 @@ CTN_DEV void dv_signal(uint32_t* f, uint32_t gen) {
 template <int NK, int NSL, int PF>
 __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
   constexpr int TM = DV_TM, KB = DV_KB, KR = DV_KR, NS = DV_NS;
-  constexpr int SLOT = dv_slot<NK>();
-  static_assert(NSL * SLOT <= 160 * 1024 - 512, "LDS budget");
+  constexpr int SLOT = DV_SLOT;
+  static_assert(NSL * SLOT <= 160 * 1024 - 2048, "LDS budget");
   __shared__ __attribute__((aligned(16))) char smem[NSL * SLOT];
   __shared__ __attribute__((aligned(16))) uint32_t fl_full[NSL][4];   // per memory wave
-  __shared__ __attribute__((aligned(16))) uint32_t fl_done[NSL][8];   // per consumer wave
+  __shared__ __attribute__((aligned(16))) uint32_t fl_done[NSL][DV_ND];   // per row / column wave
   __shared__ __attribute__((aligned(16))) float sgb[2][NS];            // gamma2 / beta2 of the slice
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -155,60 +154,45 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
   const int Kp = p.g.Kp, Kv = p.g.K, tpu = Kp / TM;
 
   if (tid < NSL * 4) (&fl_full[0][0])[tid] = 0u;
-  else if (tid < NSL * 12) (&fl_done[0][0])[tid - NSL * 4] = 0u;
+  else if (tid < NSL * (4 + DV_ND)) (&fl_done[0][0])[tid - NSL * 4] = 0u;
   if (tid < 2 * NS) sgb[tid / NS][tid % NS] = (tid < NS ? p.bop.gamma : p.bop.beta)[n0 + tid % NS];
   __syncthreads();
 
-  if (wid < DV_NC) {
-    // ======================= consumer waves =======================
-    const int w = wid;
-    // resident W fragments: fragment (group 4*sl + w/2, nb = w&1) of W (rows = output
-    // channels): lane (lg, lr) of the MFMA result then holds output channels
-    // cl .. cl+3 of frame row lr, cl = 32*(w/2) + 8*lg + 4*(w&1) (slice-local)
-    v4u wf[KB];
+  const float eal = p.alpha[0];
+  const int kmax = ws_runs_kmax(ntile, nr, tpu);
+  if (wid < DV_NR) {
+    // ======================= row waves =======================
+    // wave r: output channels n0 + 32r .. +31 of both 16-row blocks of every tile, against
+    // the resident W fragments (group 4*sl + r of the fragment-ordered copy, nb = 0, 1):
+    // lane (lg, lr) holds channels 32r + 8lg .. +7 (slice-local) of frame rows lr, 16 + lr.
+    const int r = wid;
+    v4u wf[2][KB];
     const bf16raw* WF = reinterpret_cast<const bf16raw*>(p.Wf);
     const bf16raw* W = reinterpret_cast<const bf16raw*>(p.W);
-    {
-      const int n = n0 + 32 * (w >> 1) + (lr >> 2) * 8 + (w & 1) * 4 + (lr & 3);
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const int n = n0 + 32 * r + (lr >> 2) * 8 + nb * 4 + (lr & 3);
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb)
-        wf[kb] = WF ? ldg16(WF + frag_offset(4 * sl + (w >> 1), w & 1, kb, lane, KR))
-                    : ldg16(W + (size_t)n * p.ldw + kb * 32 + lg * 8);
+        wf[nb][kb] = WF ? ldg16(WF + frag_offset(4 * sl + r, nb, kb, lane, KR))
+                        : ldg16(W + (size_t)n * p.ldw + kb * 32 + lg * 8);
     }
-    const int cl = 32 * (w >> 1) + 8 * lg + 4 * (w & 1);
-    const float4 g4 = *reinterpret_cast<const float4*>(p.gamma + n0 + cl);
-    const float eal = p.alpha[0];
-    // column part: wave (wp, wn) owns dW2 blocks p in [64 wp, +64), n in [n0 + 64 wn, +64)
-    const int wp = w >> 1, wn = w & 1;
-    f32x4_t dacc[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) dacc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-    // lane-constant LDS addresses (ctn_gemm_dual.hip's, B blocks at stride DV_BST)
+    const int cl = 32 * r + 8 * lg;
+    bf16raw* Cg = reinterpret_cast<bf16raw*>(p.C);
+    float gam[8];
+    *reinterpret_cast<float4*>(gam) = *reinterpret_cast<const float4*>(p.gamma + n0 + cl);
+    *reinterpret_cast<float4*>(gam + 4) = *reinterpret_cast<const float4*>(p.gamma + n0 + cl + 4);
     const int rbase = lg * 256 + ((lr ^ ((lg & 1) * 12)) << 4);   // + rb * KB * 1024 + kb * 1024
-    const int q = lr >> 2, pp = lr & 3;
-    int abase[2], bbase[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int row = 8 * lg + 4 * h + q;
-      abase[h] = (lg >> 1) * KB * 1024 + 2 * wp * 1024 + (pp >> 1) * 256 + (((row & 15) ^ ((pp >> 1) * 12)) << 4) +
-                 (pp & 1) * 8;
-      bbase[h] = wn * 4 * DV_BST + dv_boff(row, 4 * pp);
-    }
-    const int ro = dv_roff(lr, 4 * (w >> 1) + lg) + (w & 1) * 8;   // row lr; row 16 + lr at + 4096
+    const int ro = dv_roff(lr, 4 * r + lg);                        // row lr; row 16 + lr at + 4096
 
     double run_s = 0.0, run_q = 0.0;
     const int m0 = t0 / tpu;
     int run_m = m0;
-    const int kmax = ws_runs_kmax(ntile, nr, tpu);
-    double2* run_slab = p.grp_slab + (((size_t)rr * S + sl) * DV_NC + w) * kmax;
+    double2* run_slab = p.grp_slab + (((size_t)rr * S + sl) * DV_NR + r) * kmax;
     auto flush = [&]() __attribute__((always_inline)) {
       const double s = wave_sum_dpp_d(run_s), ss = wave_sum_dpp_d(run_q);
       run_slab[run_m - m0] = make_double2(s, ss);
     };
-
     auto run = [&](auto le1) __attribute__((always_inline)) {
       constexpr bool LE1 = decltype(le1)::value;
       int slot = 0;
@@ -217,86 +201,48 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
         dv_wait<4>(fl_full[slot], gen);
         char* base = smem + slot * SLOT;
         if constexpr (!(CTN_DV_EXP & 1)) {
-          // ---- column part first (its fragments die before the row part's accumulators
-          //      live): dW2 += gy_tile^T . op(d)_tile (reduction over the 32 rows)
-          if constexpr (!(CTN_DV_EXP & 2)) {
-            const char* a = base + OFF_A;
-            const char* bb = base + OFF_B;
-            bf16x8_t bfr[4];
+          f32x4_t acc[2][2];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const s16x4_t lo = dv_tr(bb + bbase[0] + j * DV_BST), hi = dv_tr(bb + bbase[1] + j * DV_BST);
-              bfr[j] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) acc[rb][nb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb) {
+              const v4u b = *reinterpret_cast<const v4u*>(base + OFF_A + rb * KB * 1024 + rbase + kb * 1024);
+#pragma unroll
+              for (int nb = 0; nb < 2; ++nb)
+                acc[rb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wf[nb][kb]),
+                                                                      __builtin_bit_cast(bf16x8_t, b), acc[rb][nb], 0, 0, 0);
             }
+          // ---- epilogue: norm-2 backward sums, C image (16 bytes per lane and row)
+          float s1[2] = {0.f, 0.f}, q1[2] = {0.f, 0.f};
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const int o = (i >> 1) * 1024 + (i & 1) * 512;
-              const s16x4_t lo = dv_tr(a + abase[0] + o), hi = dv_tr(a + abase[1] + o);
-              const bf16x8_t af = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          for (int rb = 0; rb < 2; ++rb) {
+            const v4u rw = *reinterpret_cast<const v4u*>(base + OFF_R + ro + rb * 4096);
+            float2 est;
+            if constexpr (NK == NORM_GLN) est = *reinterpret_cast<const float2*>(base + OFF_ST);   // the tile's utterance
+            else est = *reinterpret_cast<const float2*>(base + OFF_ST + (2 * rb + (lr >> 3)) * 256 + (lr & 7) * 8);
+            const float rs = est.y, ms = -est.x * est.y;
+            const bool ok = NK == NORM_GLN || (t * TM) % Kp + 16 * rb + lr < Kv;   // cLN padded frames: stats not finite
+            float f[8];
+            unpack_bf16x8(rw, f);
+            if constexpr (!(CTN_DV_EXP & 4)) {
 #pragma unroll
-              for (int j = 0; j < 4; ++j) dacc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], dacc[i][j], 0, 0, 0);
-            }
-          }
-          // ---- row part: both 16-row blocks against the resident W fragments
-          f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int kb = 0; kb < KB; ++kb) {
-            const v4u b0 = *reinterpret_cast<const v4u*>(base + OFF_A + rbase + kb * 1024);
-            const v4u b1 = *reinterpret_cast<const v4u*>(base + OFF_A + KB * 1024 + rbase + kb * 1024);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wf[kb]),
-                                                           __builtin_bit_cast(bf16x8_t, b0), acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wf[kb]),
-                                                           __builtin_bit_cast(bf16x8_t, b1), acc1, 0, 0, 0);
-          }
-          // ---- epilogue: norm-2 backward sums, C image
-          const uint2 r0 = *reinterpret_cast<const uint2*>(base + OFF_R + ro);
-          const uint2 r1 = *reinterpret_cast<const uint2*>(base + OFF_R + ro + 4096);
-          float2 e0, e1;
-          if constexpr (NK == NORM_GLN) {   // the tile's utterance statistics, staged by the memory waves
-            e0 = e1 = *reinterpret_cast<const float2*>(base + OFF_ST);
-          } else {
-            e0 = *reinterpret_cast<const float2*>(base + OFF_ST + lr * 8);
-            e1 = *reinterpret_cast<const float2*>(base + OFF_ST + (16 + lr) * 8);
-          }
-          f32x2_t s2[2] = {{0.f, 0.f}, {0.f, 0.f}}, q2[2] = {{0.f, 0.f}, {0.f, 0.f}};
-          if constexpr (!(CTN_DV_EXP & 4)) {
-            const f32x2_t gq[2] = {{g4.x, g4.y}, {g4.z, g4.w}};
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-              const uint2 rw = j ? r1 : r0;
-              const f32x4_t& ac = j ? acc1 : acc0;
-              const float2 est = j ? e1 : e0;
-              const f32x2_t rs = {est.y, est.y}, ms = {-est.x * est.y, -est.x * est.y};
-              const uint32_t rwv[2] = {rw.x, rw.y};
-#pragma unroll
-              for (int c = 0; c < 2; ++c) {
-                const f32x2_t x = {__uint_as_float(rwv[c] << 16), __uint_as_float(rwv[c] & 0xffff0000u)};
-                f32x2_t ah = pfma(prelu2<LE1>(x, eal), rs, ms);   // hat a
-                if constexpr (NK == NORM_CLN) {   // padded frames: statistics not finite
-                  const bool ok = (t * TM) % Kp + 16 * j + lr < Kv;
-                  ah = ok ? ah : f32x2_t{0.f, 0.f};
-                }
-                const f32x2_t ga = f32x2_t{ac[2 * c], ac[2 * c + 1]} * gq[c];
-                s2[j] += ga;
-                q2[j] = pfma(ga, ah, q2[j]);
+              for (int e = 0; e < 8; ++e) {
+                const float x = f[e];
+                const float a = LE1 ? fmaxf(x, x * eal) : fminf(x, x * eal);   // PReLU
+                const float ah = ok ? fmaf(a, rs, ms) : 0.f;                     // hat a
+                const float ga = acc[rb][e >> 2][e & 3] * gam[e];
+                s1[rb] += ga;
+                q1[rb] = fmaf(ga, ah, q1[rb]);
               }
             }
-          }
-          if constexpr (CTN_DV_DBG & 16) {
-            *reinterpret_cast<uint2*>(base + OFF_C + ro) = r0;
-            *reinterpret_cast<uint2*>(base + OFF_C + ro + 4096) = r1;
-          } else {
-            *reinterpret_cast<uint2*>(base + OFF_C + ro) = make_uint2(pk_bf16(acc0[0], acc0[1]), pk_bf16(acc0[2], acc0[3]));
-            *reinterpret_cast<uint2*>(base + OFF_C + ro + 4096) =
-                make_uint2(pk_bf16(acc1[0], acc1[1]), pk_bf16(acc1[2], acc1[3]));
-          }
-          if constexpr (CTN_DV_DBG & 4) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          if constexpr (CTN_DV_DBG & 8) {   // per-tile, per-lane sums and their inputs (debug: p.R)
-            v4u* dbg = reinterpret_cast<v4u*>(const_cast<void*>(p.R)) + ((((size_t)t * S + sl) * DV_NC + w) * 64 + lane) * 3;
-            dbg[0] = v4u{__float_as_uint((s2[0][0] + s2[0][1]) + (s2[1][0] + s2[1][1])),
-                         __float_as_uint((q2[0][0] + q2[0][1]) + (q2[1][0] + q2[1][1])), __float_as_uint(eal), 0u};
-            dbg[1] = v4u{r0.x, r0.y, r1.x, r1.y};
-            dbg[2] = v4u{__float_as_uint(e0.x), __float_as_uint(e0.y), __float_as_uint(e1.x), __float_as_uint(e1.y)};
+            const v4u cv = {pk_bf16(acc[rb][0][0], acc[rb][0][1]), pk_bf16(acc[rb][0][2], acc[rb][0][3]),
+                            pk_bf16(acc[rb][1][0], acc[rb][1][1]), pk_bf16(acc[rb][1][2], acc[rb][1][3])};
+            // whole 16-byte lanes straight to memory (a wave covers 16 rows x 64 B)
+            stg16(Cg + ((size_t)t * TM + 16 * rb + lr) * p.ldc + n0 + cl, (CTN_DV_DBG & 16) ? rw : cv);
           }
           if constexpr (NK == NORM_GLN) {
             const int m = t / tpu;
@@ -305,19 +251,20 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
               run_s = run_q = 0.0;
               run_m = m;
             }
-            run_s += (double)((s2[0][0] + s2[0][1]) + (s2[1][0] + s2[1][1]));
-            run_q += (double)((q2[0][0] + q2[0][1]) + (q2[1][0] + q2[1][1]));
+            run_s += (double)(s1[0] + s1[1]);
+            run_q += (double)(q1[0] + q1[1]);
           } else {
-            // per-row partial over this wave's 16 channels (the four lane groups), one
-            // entry per row and wave; the memory waves add the 8 waves in order
+            // per-row partial over this wave's 32 channels (the four lane groups): one
+            // entry per (row, slice, row wave), summed in that order by the finalize
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-              const float s = xsum_rows(s2[j][0] + s2[j][1]), ss = xsum_rows(q2[j][0] + q2[j][1]);
-              if (lg == 0) *reinterpret_cast<float2*>(base + OFF_PT + ((16 * j + lr) * DV_NC + w) * 8) = make_float2(s, ss);
+            for (int rb = 0; rb < 2; ++rb) {
+              const float s = xsum_rows(s1[rb]), ss = xsum_rows(q1[rb]);
+              if (lg == 0)
+                p.grp_slab[((size_t)t * TM + 16 * rb + lr) * (S * DV_NR) + sl * DV_NR + r] = make_double2((double)s, (double)ss);
             }
           }
         }
-        dv_signal(&fl_done[slot][w], gen);
+        dv_signal(&fl_done[slot][r], gen);
         if (++slot == NSL) {
           slot = 0;
           ++gen;
@@ -328,6 +275,57 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
       if (eal <= 1.f) run(std::true_type{});
       else run(std::false_type{});
       if constexpr (NK == NORM_GLN) flush();
+    }
+    return;
+  }
+  if (wid < DV_NR + DV_NC) {
+    // ======================= column waves =======================
+    // wave c = (wp, wn) owns dW2 blocks p in [64 wp, +64), n in [n0 + 64 wn, +64):
+    // dW2 += gy_tile^T . op(d)_tile, the reduction over the tile's 32 frame rows
+    const int c = wid - DV_NR, wp = c >> 1, wn = c & 1;
+    f32x4_t dacc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dacc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    // lane-constant LDS addresses (ctn_gemm_dual.hip's, B blocks at stride DV_BST)
+    const int q = lr >> 2, pp = lr & 3;
+    int abase[2], bbase[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int row = 8 * lg + 4 * h + q;
+      abase[h] = (lg >> 1) * KB * 1024 + 2 * wp * 1024 + (pp >> 1) * 256 + (((row & 15) ^ ((pp >> 1) * 12)) << 4) +
+                 (pp & 1) * 8;
+      bbase[h] = wn * 4 * DV_BST + dv_boff(row, 4 * pp);
+    }
+    int slot = 0;
+    uint32_t gen = 1;
+    for (int t = t0; t < t1; ++t) {
+      dv_wait<4>(fl_full[slot], gen);
+      const char* base = smem + slot * SLOT;
+      if constexpr (!(CTN_DV_EXP & 3)) {
+        const char* a = base + OFF_A;
+        const char* bb = base + OFF_B;
+        bf16x8_t bfr[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const s16x4_t lo = dv_tr(bb + bbase[0] + j * DV_BST), hi = dv_tr(bb + bbase[1] + j * DV_BST);
+          bfr[j] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int o = (i >> 1) * 1024 + (i & 1) * 512;
+          const s16x4_t lo = dv_tr(a + abase[0] + o), hi = dv_tr(a + abase[1] + o);
+          const bf16x8_t af = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) dacc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], dacc[i][j], 0, 0, 0);
+        }
+      }
+      dv_signal(&fl_done[slot][DV_NR + c], gen);
+      if (++slot == NSL) {
+        slot = 0;
+        ++gen;
+      }
     }
     // dW2 partial of this workgroup: lane holds D[(wp*4+i)*16 + 4lg + e][n0 + (wn*4+j)*16 + lr]
     float* Dp = p.Dpart + (size_t)rr * KR * p.Nout;
@@ -343,145 +341,103 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
   }
 
   // ======================= memory waves =======================
-  const int mw = wid - DV_NC;
-  bf16raw* C = reinterpret_cast<bf16raw*>(p.C);
-  // A: blocks f = 4*mw + u of the tile (row block f/8, k-block f%8): lane -> row, chunk
-  //    such that the wave's 64 x 16 bytes fill the 1-KiB block contiguously
-  // buffer loads: per-lane 32-bit byte offsets, the tile's row offset in an SGPR
+  // Memory wave m moves, per tile, A blocks 4m..4m+3 (16 rows x 32 channels of gy each),
+  // raw-d pieces 2m, 2m+1 (4 rows x the slice's 128 channels each) and its statistics
+  // piece by LDS-DMA (buffer_load ... lds: no registers, PF tiles ahead), waits for its
+  // own DMA group with a counted vmcnt (no other memory operations are issued by these
+  // waves), reads back its own raw-d pieces to write op(d) into the B image, and
+  // publishes FULL.  A slot is refilled only after every row / column wave's DONE for the
+  // tile that used it last.
+  const int mw = wid - DV_ND;
   const rsrc_t rA = du_rsrc(p.A, rows * p.lda * 2), rD = du_rsrc(p.Bm, rows * p.ldb * 2);
+  const rsrc_t rS = du_rsrc(p.bop.stats, (NK == NORM_GLN ? (long)p.g.M : rows) * 8);
   int arow[4];
   uint32_t aoff[4];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
+  for (int u = 0; u < 4; ++u) {   // lane L lands at block + 16 L: the fragment-order image
     const int f = 4 * mw + u, mb = f / KB, kb = f % KB;
     arow[u] = 16 * mb + ((lane & 15) ^ (((lane >> 4) & 1) * 12));
     aoff[u] = (uint32_t)(arow[u] * p.lda + (4 * kb + (lane >> 4)) * 8) * 2u;
   }
-  // d / C: row dr = 8*mw + lane/8, chunks c = 8h + lane%8 (each 8 lanes: one 128-byte run)
-  const int dr = 8 * mw + (lane >> 3);
-  int cch[2], roff[2], boff[2];
+  // raw-d piece i = 2*mw + h: row 4i + L/16, granule position L%16 holds channels
+  // 8g .. 8g+7, g = (L%16) ^ (row%16) (the R image's swizzle, applied on the source)
+  int drow[2], dgr[2], boff[2];
   uint32_t doff[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    cch[h] = 8 * h + (lane & 7);
-    roff[h] = dv_roff(dr, cch[h]);
-    boff[h] = (cch[h] >> 1) * DV_BST + dv_boff(dr, 8 * (cch[h] & 1));
-    doff[h] = (uint32_t)(dr * p.ldb + n0 + 8 * cch[h]) * 2u;
+    drow[h] = 4 * (2 * mw + h) + (lane >> 4);
+    dgr[h] = (lane & 15) ^ (drow[h] & 15);
+    doff[h] = (uint32_t)(drow[h] * p.ldb + n0 + 8 * dgr[h]) * 2u;
+    boff[h] = (dgr[h] >> 1) * DV_BST + dv_boff(drow[h], 8 * (dgr[h] & 1));
   }
+  // statistics piece: cLN rows 8m .. 8m+7 (lanes 0..15, one dword each); gLN the tile's
+  // utterance pair (wave 0, lanes 0..1); other lanes read out of range (zeros) into the
+  // wave's own 256 bytes
+  const bool st_lane = NK == NORM_CLN ? lane < 16 : (mw == 0 && lane < 2);
+  const uint32_t soff = st_lane ? (uint32_t)((NK == NORM_CLN ? 8 * mw * 8 : 0) + lane * 4) : DU_OOB;
   const float bal = p.bop.alpha[0];
+  constexpr int G = 7;   // DMA instructions per wave and tile
 
-  v4u ra[PF][4], rd[PF][2];
-  float2 rst[PF];
-  // (the padded-frame zeroing of gy waits until write(): a select here would wait for
-  // the load just issued)
-  auto load = [&](int t, auto s) __attribute__((always_inline)) {
-    constexpr int si = decltype(s)::value;
-    const size_t r0 = (size_t)t * TM;
-    const int sa = t * TM * p.lda * 2, sd = t * TM * p.ldb * 2;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) ra[si][u] = __builtin_amdgcn_raw_buffer_load_b128(rA, aoff[u], sa, 0);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) rd[si][h] = __builtin_amdgcn_raw_buffer_load_b128(rD, doff[h], sd, 0);
-    // statistics with the tile's operands (a load issued at its point of use would be the
-    // youngest in the wave's in-order vmcnt queue and drain the prefetch)
-    rst[si] = p.bop.stats[NK == NORM_GLN ? (size_t)(t / tpu) : r0 + dr];
-  };
-  // store the C image (and the cLN per-row sums) of tile tc from slot `base`
-  auto store_c = [&](int tc, const char* base) __attribute__((always_inline)) {
-    const size_t r0 = (size_t)tc * TM;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const v4u v = *reinterpret_cast<const v4u*>(base + OFF_C + roff[h]);
-      stg16(C + (r0 + dr) * p.ldc + n0 + 8 * cch[h], v);
-    }
-    if constexpr (NK == NORM_CLN) {
-      if ((lane & 7) == 0) {
-        double s = 0.0, ss = 0.0;
-#pragma unroll
-        for (int i = 0; i < DV_NC; ++i) {
-          const float2 v = *reinterpret_cast<const float2*>(base + OFF_PT + (dr * DV_NC + i) * 8);
-          s += (double)v.x;
-          ss += (double)v.y;
-        }
-        p.grp_slab[(r0 + dr) * S + sl] = make_double2(s, ss);
-      }
-    }
-  };
-  auto write = [&](auto le1, int t, char* base, auto s) __attribute__((always_inline)) {
-    constexpr bool LE1 = decltype(le1)::value;
-    constexpr int si = decltype(s)::value;
+  auto dma = [&](int t) __attribute__((always_inline)) {
+    char* base = smem + ((t - t0) % NSL) * SLOT;
     const int tk = (t * TM) % Kp;
 #pragma unroll
-    for (int u = 0; u < 4; ++u)   // padded frames: zero gy rows
-      stg16(base + OFF_A + (4 * mw + u) * 1024 + lane * 16, tk + arow[u] < Kv ? ra[si][u] : v4u{0u, 0u, 0u, 0u});
-    const float2 st = rst[si];
-    const bool ok = NK == NORM_GLN || (t * TM) % Kp + dr < Kv;
-    const f32x2_t m2 = {st.x, st.x};
+    for (int u = 0; u < 4; ++u)   // rows of padded frames arrive as zeros (out-of-range offset)
+      du_dma16(rA, base + OFF_A + (4 * mw + u) * 1024, tk + arow[u] < Kv ? aoff[u] : DU_OOB, t * TM * p.lda * 2);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) du_dma16(rD, base + OFF_R + (2 * mw + h) * 1024, doff[h], t * TM * p.ldb * 2);
+    du_dma4(rS, base + OFF_ST + mw * 256, soff, NK == NORM_GLN ? (t / tpu) * 8 : t * TM * 8);
+  };
+  auto transform = [&](auto le1, int t, char* base) __attribute__((always_inline)) {
+    constexpr bool LE1 = decltype(le1)::value;
+    const int tk = (t * TM) % Kp;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      v4u v = rd[si][h];
-      if constexpr (!(CTN_DV_DBG & 2)) stg16(base + OFF_R + roff[h], v);
-      if constexpr (CTN_DV_DBG & 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const int row = drow[h];
+      v4u v = *reinterpret_cast<const v4u*>(base + OFF_R + (2 * mw + h) * 1024 + lane * 16);
+      const float2 st = *reinterpret_cast<const float2*>(base + OFF_ST + (NK == NORM_GLN ? 0 : mw * 256 + (row & 7) * 8));
       float gam[8], bet[8];
-      *reinterpret_cast<float4*>(gam) = *reinterpret_cast<const float4*>(&sgb[0][8 * cch[h]]);
-      *reinterpret_cast<float4*>(gam + 4) = *reinterpret_cast<const float4*>(&sgb[0][8 * cch[h] + 4]);
-      *reinterpret_cast<float4*>(bet) = *reinterpret_cast<const float4*>(&sgb[1][8 * cch[h]]);
-      *reinterpret_cast<float4*>(bet + 4) = *reinterpret_cast<const float4*>(&sgb[1][8 * cch[h] + 4]);
+      *reinterpret_cast<float4*>(gam) = *reinterpret_cast<const float4*>(&sgb[0][8 * dgr[h]]);
+      *reinterpret_cast<float4*>(gam + 4) = *reinterpret_cast<const float4*>(&sgb[0][8 * dgr[h] + 4]);
+      *reinterpret_cast<float4*>(bet) = *reinterpret_cast<const float4*>(&sgb[1][8 * dgr[h]]);
+      *reinterpret_cast<float4*>(bet + 4) = *reinterpret_cast<const float4*>(&sgb[1][8 * dgr[h] + 4]);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        f32x2_t x = {__uint_as_float(v[e] << 16), __uint_as_float(v[e] & 0xffff0000u)};
-        x = prelu2<LE1>(x, bal);
-        x = pfma(x - m2, f32x2_t{st.y * gam[2 * e], st.y * gam[2 * e + 1]}, f32x2_t{bet[2 * e], bet[2 * e + 1]});
-        v[e] = pk_bf16(x[0], x[1]);
+        float x0 = __uint_as_float(v[e] << 16), x1 = __uint_as_float(v[e] & 0xffff0000u);
+        x0 = LE1 ? fmaxf(x0, x0 * bal) : fminf(x0, x0 * bal);   // PReLU
+        x1 = LE1 ? fmaxf(x1, x1 * bal) : fminf(x1, x1 * bal);
+        x0 = fmaf(x0 - st.x, st.y * gam[2 * e], bet[2 * e]);
+        x1 = fmaf(x1 - st.x, st.y * gam[2 * e + 1], bet[2 * e + 1]);
+        v[e] = pk_bf16(x0, x1);
       }
-      if constexpr (NK == NORM_CLN) v = ok ? v : v4u{0u, 0u, 0u, 0u};
+      if constexpr (NK == NORM_CLN)   // padded frames: statistics not finite
+        if (tk + row >= Kv) v = v4u{0u, 0u, 0u, 0u};
       stg16(base + OFF_B + boff[h], v);
     }
-    if constexpr (CTN_DV_DBG & 2) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        v4u v = rd[si][h];
-        asm volatile("" : "+v"(v));
-        stg16(base + OFF_R + roff[h], v);
-        if constexpr (CTN_DV_DBG & 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  auto run = [&](auto le1) __attribute__((always_inline)) {
+    for (int i = 0; i < PF; ++i)
+      if (t0 + i < t1) dma(t0 + i);
+    int slot = 0;
+    uint32_t gen = 1;
+    for (int t = t0; t < t1; ++t) {
+      const int later = t1 - 1 - t < PF - 1 ? t1 - 1 - t : PF - 1;   // DMA groups issued after tile t's
+      vmwait23(G * later);
+      char* base = smem + slot * SLOT;
+      transform(le1, t, base);
+      dv_signal(&fl_full[slot][mw], gen);
+      const int tn = t + PF;
+      if (tn < t1) {
+        const int kn = tn - t0;   // its slot was last used by tile tn - NSL: wait for every DONE of it
+        dv_wait<DV_ND>(fl_done[kn % NSL], (uint32_t)(kn / NSL));
+        dma(tn);
+      }
+      if (++slot == NSL) {
+        slot = 0;
+        ++gen;
       }
     }
-    if constexpr (NK == NORM_CLN) {
-      if ((lane & 7) == 0) *reinterpret_cast<float2*>(base + OFF_ST + dr * 8) = st;
-    } else {
-      if (mw == 0 && lane == 0) *reinterpret_cast<float2*>(base + OFF_ST) = st;
-    }
-  };
-
-  auto run = [&](auto le1) __attribute__((always_inline)) {
-    // Loads are issued unconditionally (tiles past the range clamped to its last one,
-    // loaded and never used): the compiler's vmcnt bookkeeping then sees the same queue
-    // on every path, and each wait leaves the later tiles' loads in flight.
-    auto clampt = [&](int t) __attribute__((always_inline)) { return t < t1 ? t : t1 - 1; };
-    static_for<PF>([&](auto s) { load(clampt(t0 + decltype(s)::value), s); });
-    for (int tb = t0; tb < t1; tb += PF) {
-      static_for<PF>([&](auto s) {
-        const int t = tb + decltype(s)::value;
-        if (t < t1) {
-          const int k = t - t0, slot = k % NSL;
-          const uint32_t gen = (uint32_t)(k / NSL) + 1;
-          char* base = smem + slot * SLOT;
-          if (k >= NSL) {   // the consumers are done with tile t - NSL: store its C image
-            dv_wait<8>(fl_done[slot], gen - 1);
-            store_c(t - NSL, base);
-          }
-          write(le1, t, base, s);
-          dv_signal(&fl_full[slot][mw], gen);
-        }
-        load(clampt(t + PF), s);
-      });
-    }
-    // the last NSL tiles' C images
-    for (int t = (t1 - NSL > t0 ? t1 - NSL : t0); t < t1; ++t) {
-      const int k = t - t0, slot = k % NSL;
-      dv_wait<8>(fl_done[slot], (uint32_t)(k / NSL) + 1);
-      store_c(t, smem + slot * SLOT);
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may land after the wave ends
   };
   if (t0 < t1) {
     if (bal <= 1.f) run(std::true_type{});
@@ -522,9 +478,9 @@ hipError_t launch_gemm_dual_ws(const GemmDual& p, hipStream_t s) {
   if (!gemm_dual_ws_eligible(p)) return hipErrorInvalidValue;
   const dim3 grid(gemm_dual_ws_ranges(p) * (p.Nout / DV_NS));
   if (p.norm == NORM_GLN)
-    hipLaunchKernelGGL((gemm_dual_ws_kernel<NORM_GLN, 3, 3>), grid, dim3(DV_NT), 0, s, p);
+    hipLaunchKernelGGL((gemm_dual_ws_kernel<NORM_GLN, DV_NSL, DV_NSL - 1>), grid, dim3(DV_NT), 0, s, p);
   else
-    hipLaunchKernelGGL((gemm_dual_ws_kernel<NORM_CLN, 3, 3>), grid, dim3(DV_NT), 0, s, p);
+    hipLaunchKernelGGL((gemm_dual_ws_kernel<NORM_CLN, DV_NSL, DV_NSL - 1>), grid, dim3(DV_NT), 0, s, p);
   return hipGetLastError();
 }
 

@@ -112,7 +112,6 @@ CTN_DEV s16x4_t du_tr(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(p));
 }
 
-constexpr uint32_t DU_OOB = 0x80000000u;   // voffset past every buffer: loads return 0
 
 // NV consecutive bf16 (NV = 4: 8-byte access, NV = 8: 16-byte access) through a buffer resource
 template <int NV> struct DuVec { uint32_t w[NV / 2]; };
@@ -636,7 +635,7 @@ WsRuns gemm_dual_runs(const GemmDual& p) {
   w.ntile = (int)(p.g.rows() / DU_TM);
   w.grid = gemm_dual_ranges(p);
   w.tpu = p.g.Kp / DU_TM;
-  w.waves = dual_slices(p) * DU_WV;
+  w.waves = dual_slices(p) * (gemm_dual_ws_eligible(p) ? 4 : DU_WV);   // ctn_dual_ws.hip: 4 row waves
   w.kmax = ws_runs_kmax(w.ntile, w.grid, w.tpu);
   return w;
 }
@@ -644,7 +643,7 @@ WsRuns gemm_dual_runs(const GemmDual& p) {
 int gemm_dual_group_parts(const GemmDual& p) {
   int kb, nsb, nbw;
   dual_shape(p.Kred, p.Nout, &kb, &nsb, &nbw);
-  if (p.norm != NORM_GLN) return gemm_dual_ws_eligible(p) ? dual_slices(p) : dual_slices(p) * (nsb / nbw);
+  if (p.norm != NORM_GLN) return dual_slices(p) * (gemm_dual_ws_eligible(p) ? 4 : nsb / nbw);   // per (slice, row wave)
   const WsRuns w = gemm_dual_runs(p);
   const long entries = (long)w.grid * w.waves * w.kmax;
   return (int)((entries + p.g.M - 1) / p.g.M);

@@ -315,9 +315,17 @@ struct StreamArgs {
   float* frames;                 // decode scratch [M][C][K][L]
   float* tail_out;               // [M][C][L/2]
   float* out;                    // [M][C][K*L/2]
+  // ABI v7 call path (launch_stream_call_stage): norm-2 parameters and W2 of a block
+  const float* na2 = nullptr;
+  const float* nb2 = nullptr;
+  const float* W2 = nullptr;
 };
 // which: 0 encode, 1 block in (1x1, PReLU, norm 1 -> ring), 2 block out (depthwise, PReLU,
 // norm 2, 1x1, residual), 3 decode (mask, sources, frames, overlap-add)
 hipError_t launch_stream(int which, const StreamArgs& a, hipStream_t s);
+// ABI v7 (ctn_stream_call): 0 encode, 1 block in (W1 chunks -> h1 scratch in `frames`),
+// 2 block out (taps, depthwise, norms, W2 chunks, residual, ring), 3 decode mask
+// (-> sources in `frames`), 4 decoder basis + overlap-add
+hipError_t launch_stream_call_stage(int which, const StreamArgs& a, hipStream_t s);
 
 }  // namespace ctn

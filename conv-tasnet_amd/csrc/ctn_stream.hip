@@ -282,6 +282,234 @@ __global__ __launch_bounds__(ST_NT) void stream_ola_kernel(StreamArgs a) {
   }
 }
 
+// ===========================================================================
+// ABI v7 call path (ctn_stream_call): the same arithmetic cut over many workgroups.
+// The v5 kernels above give each (stream, 8 frames) ONE workgroup, which streams a
+// whole 1x1 weight (0.5 MiB fp32) through one CU: ~50 us per launch whatever the
+// chunk size.  Here every 1x1 conv is split over 32-output column chunks (each
+// workgroup reads a 32-column slice of the weight), and the per-frame norms that need
+// a whole row are recomputed by every chunk workgroup of that frame (same arithmetic,
+// same order: every copy is bit-identical).
+//   SE  encode + cLN + bottleneck chunk              grid (M, frame groups, B/32)
+//   SA  block: W1 chunk -> h1 (pre-PReLU) scratch     grid (M, frame groups, H/32)
+//   SB  block: taps (ring for frames of earlier calls, PReLU + norm 1 of h1 rows of
+//       this call), depthwise, PReLU, norm 2, W2 chunk + residual; chunk 0 writes the
+//       frame's norm-1 row to the ring                 grid (M, K, B/32)
+//   SD1 mask 1x1 chunk (all speakers of 32 channels), nonlinearity, * w -> sources
+//   SD2 sources . V^T -> frames, overlap-add with the carried tail
+// ===========================================================================
+constexpr int SC_W = 32;                 // outputs per chunk workgroup
+constexpr int SC_SL = ST_NT / SC_W;      // input slices per output (8)
+constexpr int SC_FPB = 8;                // frames per workgroup (SE, SA, SD1)
+
+// res[f] (valid in threads t < SC_W) = sum_i Wt[i][j0 + t] * in[f][i]; thread (o, s) sums
+// the inputs i = s, s + 8, ... (a 128-byte weight row segment per 32 threads), then the
+// 8 slices are added in order.  red: SC_FPB * ST_NT floats.
+template <int F>
+CTN_DEV void sc_matvec(const float* __restrict__ Wt, int n_in, int n_out, int j0, const float* in, int ld_in, int nf,
+                       float (&res)[F], float* red) {
+  const int t = threadIdx.x, o = t % SC_W, sl = t / SC_W, j = j0 + o;
+  float acc[F];
+#pragma unroll
+  for (int f = 0; f < F; ++f) acc[f] = 0.f;
+  if (j < n_out) {
+#pragma unroll 4
+    for (int i = sl; i < n_in; i += SC_SL) {
+      const float w = Wt[(size_t)i * n_out + j];
+#pragma unroll
+      for (int f = 0; f < F; ++f)
+        if (f < nf) acc[f] = fmaf(w, in[f * ld_in + i], acc[f]);
+    }
+  }
+#pragma unroll
+  for (int f = 0; f < F; ++f) red[(f * SC_SL + sl) * SC_W + o] = acc[f];
+  __syncthreads();
+  if (t < SC_W) {
+#pragma unroll
+    for (int f = 0; f < F; ++f) {
+      float v = 0.f;
+#pragma unroll
+      for (int q = 0; q < SC_SL; ++q) v += red[(f * SC_SL + q) * SC_W + t];
+      res[f] = v;
+    }
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(ST_NT) void sc_encode_kernel(StreamArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int N = a.N, L = a.L, S = a.L / 2, Bc = a.B;
+  const int m = blockIdx.x, f0 = blockIdx.y * SC_FPB, nf = min(SC_FPB, a.K - f0), j0 = blockIdx.z * SC_W;
+  float* smp = sm;                                          // (FPB-1)*S + L samples
+  float* y = smp + ((SC_FPB - 1) * S + L + 3) / 4 * 4;      // [FPB][N]
+  float* red = y + SC_FPB * N;                              // [FPB][256]
+  const int ns = (nf - 1) * S + L;
+  for (int i = threadIdx.x; i < ns; i += ST_NT) smp[i] = a.samples[(size_t)m * a.ld_samples + (size_t)f0 * S + i];
+  __syncthreads();
+  for (int n = threadIdx.x; n < N; n += ST_NT)
+    for (int f = 0; f < nf; ++f) {
+      float acc = 0.f;
+      for (int l = 0; l < L; ++l) acc = fmaf(a.U[(size_t)n * L + l], smp[f * S + l], acc);
+      acc = acc > 0.f ? acc : 0.f;                          // ReLU (conv_tasnet.py:117)
+      y[f * N + n] = acc;
+      if (blockIdx.z == 0) a.w_out[((size_t)m * a.K + f0 + f) * N + n] = acc;
+    }
+  __syncthreads();
+  st_norm_rows<SC_FPB>(y, N, nf, N, 1, a.na, a.nb, red);   // separator cLN (always channel-wise)
+  float res[SC_FPB];
+  sc_matvec<SC_FPB>(a.W, N, Bc, j0, y, N, nf, res, red);
+  if (threadIdx.x < SC_W && j0 + (int)threadIdx.x < Bc)
+    for (int f = 0; f < nf; ++f) a.x_out[((size_t)m * a.K + f0 + f) * Bc + j0 + threadIdx.x] = res[f];
+}
+
+__global__ __launch_bounds__(ST_NT) void sc_block_in_kernel(StreamArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int Bc = a.B, H = a.H;
+  const int m = blockIdx.x, f0 = blockIdx.y * SC_FPB, nf = min(SC_FPB, a.K - f0), j0 = blockIdx.z * SC_W;
+  float* xs = sm;                      // [FPB][B]
+  float* red = xs + SC_FPB * Bc;
+  for (int i = threadIdx.x; i < nf * Bc; i += ST_NT) xs[i] = a.x_in[((size_t)m * a.K + f0) * Bc + i];
+  __syncthreads();
+  float res[SC_FPB];
+  sc_matvec<SC_FPB>(a.W, Bc, H, j0, xs, Bc, nf, res, red);
+  if (threadIdx.x < SC_W && j0 + (int)threadIdx.x < H)
+    for (int f = 0; f < nf; ++f) a.frames[((size_t)m * a.K + f0 + f) * H + j0 + threadIdx.x] = res[f];   // h1 scratch
+}
+
+__global__ __launch_bounds__(ST_NT) void sc_block_out_kernel(StreamArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int Bc = a.B, H = a.H, P = a.P, dil = a.dil;
+  const int m = blockIdx.x, f = blockIdx.y, j0 = blockIdx.z * SC_W;
+  float* taps = sm;                    // [P][H]: norm-1 output rows of the P taps
+  float* d = taps + P * H;             // [H]
+  float* red = d + H;                  // [ST_NT * SC_FPB]
+  const unsigned mask = (unsigned)a.R - 1u;
+  const long g = a.pos + f;
+  const float al1 = a.alpha1[0], al2 = a.alpha2[0];
+  for (int p = 0; p < P; ++p) {
+    const long src = g - (long)(P - 1 - p) * dil;           // causal taps (conv_tasnet.py:176, Chomp1d)
+    float* row = taps + p * H;
+    if (src < a.pos) {                                       // an earlier call's frame (ring) or before the start
+      for (int j = threadIdx.x; j < H; j += ST_NT)
+        row[j] = src >= 0 ? a.ring[((size_t)m * a.R + ((unsigned)src & mask)) * H + j] : 0.f;
+      __syncthreads();
+    } else {                                                 // this call's frame: PReLU 1 + norm 1 of its h1 row
+      const float* h = a.frames + ((size_t)m * a.K + (src - a.pos)) * H;
+      for (int j = threadIdx.x; j < H; j += ST_NT) {
+        const float v = h[j];
+        row[j] = v > 0.f ? v : al1 * v;
+      }
+      __syncthreads();
+      st_norm_rows<1>(row, H, 1, H, a.norm, a.na, a.nb, red);
+    }
+  }
+  if (blockIdx.z == 0) {                                     // the frame's own norm-1 row -> its ring slot
+    float* dst = a.ring + ((size_t)m * a.R + ((unsigned)g & mask)) * H;
+    for (int j = threadIdx.x; j < H; j += ST_NT) dst[j] = taps[(P - 1) * H + j];
+  }
+  for (int j = threadIdx.x; j < H; j += ST_NT) {
+    float s = 0.f;
+    for (int p = 0; p < P; ++p) s = fmaf(a.wd[(size_t)j * P + p], taps[p * H + j], s);
+    d[j] = s > 0.f ? s : al2 * s;                            // PReLU 2
+  }
+  __syncthreads();
+  st_norm_rows<1>(d, H, 1, H, a.norm, a.na2, a.nb2, red);
+  float res[1];
+  sc_matvec<1>(a.W2, H, Bc, j0, d, H, 1, res, red);
+  if (threadIdx.x < SC_W && j0 + (int)threadIdx.x < Bc) {
+    const size_t o = ((size_t)m * a.K + f) * Bc + j0 + threadIdx.x;
+    a.x_out[o] = res[0] + a.x_in[o];                         // + residual
+  }
+}
+
+// sources[m][c][k][n] = w * mask: the mask 1x1 for all speakers of 32 channels n, then
+// the nonlinearity across speakers (conv_tasnet.py:185, 202-207, 137)
+__global__ __launch_bounds__(ST_NT) void sc_decode_mask_kernel(StreamArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int Bc = a.B, N = a.N, C = a.C, CN = C * N;
+  const int m = blockIdx.x, f0 = blockIdx.y * SC_FPB, nf = min(SC_FPB, a.K - f0), n0 = blockIdx.z * SC_W;
+  float* xs = sm;                      // [FPB][B]
+  float* sc = xs + SC_FPB * Bc;        // [C][FPB][32]
+  float* red = sc + C * SC_FPB * SC_W;
+  for (int i = threadIdx.x; i < nf * Bc; i += ST_NT) xs[i] = a.x_in[((size_t)m * a.K + f0) * Bc + i];
+  __syncthreads();
+  for (int c = 0; c < C; ++c) {
+    float res[SC_FPB];
+    sc_matvec<SC_FPB>(a.W, Bc, CN, c * N + n0, xs, Bc, nf, res, red);
+    if (threadIdx.x < SC_W)
+      for (int f = 0; f < SC_FPB; ++f) sc[(c * SC_FPB + f) * SC_W + threadIdx.x] = res[f];
+  }
+  __syncthreads();
+  const int t = threadIdx.x, n = n0 + t;
+  if (t < SC_W && n < N)
+    for (int f = 0; f < nf; ++f) {
+      const float wv = a.w_in[((size_t)m * a.K + f0 + f) * N + n];
+      float v[8];
+      for (int c = 0; c < C; ++c) v[c] = sc[(c * SC_FPB + f) * SC_W + t];
+      if (a.mask_type == 1) {
+        float mx = -3.4e38f, den = 0.f;
+        for (int c = 0; c < C; ++c) mx = fmaxf(mx, v[c]);
+        for (int c = 0; c < C; ++c) { v[c] = expf(v[c] - mx); den += v[c]; }
+        for (int c = 0; c < C; ++c) v[c] = wv * (v[c] / den);
+      } else if (a.mask_type == 0) {
+        for (int c = 0; c < C; ++c) v[c] = wv * (v[c] > 0.f ? v[c] : 0.f);
+      } else {
+        for (int c = 0; c < C; ++c) v[c] = wv * v[c];
+      }
+      for (int c = 0; c < C; ++c) a.frames[(((size_t)m * C + c) * a.K + f0 + f) * N + n] = v[c];
+    }
+}
+
+// frames = sources . V^T (decoder basis, conv_tasnet.py:138-140), then the overlap-add with
+// the previous call's tail (utils.py:9-46, L = 2S): one workgroup per (stream, speaker)
+__global__ __launch_bounds__(ST_NT) void sc_decode_ola_kernel(StreamArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int N = a.N, L = a.L, S = a.L / 2, K = a.K;
+  const int mc = blockIdx.x;
+  float* fr = sm;                      // [K][L]
+  const float* src = a.frames + (size_t)mc * K * N;
+  for (int o = threadIdx.x; o < K * L; o += ST_NT) {
+    const int k = o / L, l = o % L;
+    float acc = 0.f;
+    for (int n = 0; n < N; ++n) acc = fmaf(src[(size_t)k * N + n], a.V[(size_t)l * N + n], acc);
+    fr[o] = acc;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < K * S; i += ST_NT) {
+    const int k = i / S, s2 = i % S;
+    const float prev = k > 0 ? fr[(k - 1) * L + S + s2] : a.tail_in[(size_t)mc * S + s2];
+    a.out[(size_t)mc * K * S + i] = fr[k * L + s2] + prev;
+  }
+  for (int s2 = threadIdx.x; s2 < S; s2 += ST_NT) a.tail_out[(size_t)mc * S + s2] = fr[(K - 1) * L + S + s2];
+}
+
+size_t stream_call_smem(int which, const StreamArgs& a) {
+  const int S = a.L / 2;
+  switch (which) {
+    case 0: return (size_t)(((SC_FPB - 1) * S + a.L + 3) / 4 * 4 + SC_FPB * a.N + SC_FPB * ST_NT) * 4;
+    case 1: return (size_t)(SC_FPB * a.B + SC_FPB * ST_NT) * 4;
+    case 2: return (size_t)(a.P * a.H + a.H + SC_FPB * ST_NT) * 4;
+    case 3: return (size_t)(SC_FPB * a.B + a.C * SC_FPB * SC_W + SC_FPB * ST_NT) * 4;
+    default: return (size_t)a.K * a.L * 4;
+  }
+}
+
+hipError_t launch_stream_call_stage(int which, const StreamArgs& a, hipStream_t s) {
+  const size_t lds = stream_call_smem(which, a);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  const unsigned fg = (unsigned)((a.K + SC_FPB - 1) / SC_FPB);
+  const dim3 b(ST_NT);
+  switch (which) {
+    case 0: hipLaunchKernelGGL(sc_encode_kernel, dim3(a.M, fg, (a.B + SC_W - 1) / SC_W), b, lds, s, a); break;
+    case 1: hipLaunchKernelGGL(sc_block_in_kernel, dim3(a.M, fg, (a.H + SC_W - 1) / SC_W), b, lds, s, a); break;
+    case 2: hipLaunchKernelGGL(sc_block_out_kernel, dim3(a.M, a.K, (a.B + SC_W - 1) / SC_W), b, lds, s, a); break;
+    case 3: hipLaunchKernelGGL(sc_decode_mask_kernel, dim3(a.M, fg, (a.N + SC_W - 1) / SC_W), b, lds, s, a); break;
+    case 4: hipLaunchKernelGGL(sc_decode_ola_kernel, dim3(a.M * a.C), b, lds, s, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 size_t stream_smem(int which, const StreamArgs& a) {
   const int S = a.L / 2;
   switch (which) {

@@ -14,7 +14,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CTN_HIP_LIB", os.path.join(_HERE, "libctn_hip.so"))
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 DTYPE_F32, DTYPE_BF16 = 0, 1
 NORM_GLN, NORM_CLN, NORM_BN = 0, 1, 2
@@ -77,6 +77,19 @@ class RowsDesc(ctypes.Structure):
 
 class StreamDesc(ctypes.Structure):
     _fields_ = [(n, c_int32) for n in ("M", "K", "N", "L", "B", "H", "P", "C", "norm", "mask_type")]
+
+
+class StreamBlockParams(ctypes.Structure):
+    """ctn_stream_block_params (include/ctn.h, ABI v7)."""
+    _fields_ = [("dilation", c_int32), ("ring_frames", c_int32)] + [
+        (n, c_void_p) for n in ("w1_t", "alpha1", "norm1_a", "norm1_b", "wd", "alpha2", "norm2_a", "norm2_b", "w2_t",
+                                "ring")]
+
+
+class StreamModel(ctypes.Structure):
+    """ctn_stream_model (include/ctn.h, ABI v7): `blocks` points to a host array."""
+    _fields_ = [(n, c_void_p) for n in ("U", "gamma0", "beta0", "wb_t", "wm_t", "V", "blocks")] + [
+        ("nblocks", c_int32)]
 
 
 class OptSegment(ctypes.Structure):
@@ -146,6 +159,9 @@ _SIGS = {
     "ctn_stream_block": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int] + [c_void_p] * 12 +
                          [c_void_p]),
     "ctn_stream_decode": (ctypes.c_int, [c_void_p] + [c_void_p] * 8 + [c_void_p]),
+    "ctn_stream_workspace_bytes": (c_size_t, [c_void_p]),
+    "ctn_stream_call": (ctypes.c_int, [c_void_p, c_void_p, ctypes.c_int64, c_void_p, ctypes.c_int64] + [c_void_p] * 4 +
+                        [c_size_t, c_void_p]),
     "ctn_timer_enable": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "ctn_timer_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
 }

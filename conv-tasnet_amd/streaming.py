@@ -19,9 +19,10 @@ State kept between chunks (all on the device, fp32), nothing re-run:
 * ``tail``: the last L/2 overlap-add samples of the previous chunk.
 
 Per chunk of K new frames (cut into calls of at most ``max_frames``): one
-encode call, two kernels per TemporalBlock, one decode call (include/ctn.h
-``ctn_stream_*``, csrc/ctn_stream.hip) — work proportional to the NEW frames
-only, no padding of a call to 128-frame tiles.  Forward only (torch.no_grad);
+``ctn_stream_call`` (include/ctn.h ABI v7, csrc/ctn_stream.hip): an encode kernel,
+two kernels per TemporalBlock and two decode kernels, every 1x1 conv split over
+32-output column chunks so a call with one new frame still spreads over many CUs —
+work proportional to the NEW frames only, no padding of a call to 128-frame tiles.  Forward only (torch.no_grad);
 the weights are snapshotted (transposed 1x1 weights, folded BatchNorm) when the
 streamer is built or ``refresh_weights()`` is called.
 """
@@ -75,6 +76,8 @@ class StreamingSeparator:
         self.norm = norm
         self.stride = model.L // 2
         self.max_frames = int(max_frames)
+        # one ctn_stream_call per chunk (ABI v7); False: the v5 per-stage entries
+        self.one_call = True
         self.lib = L.load()
         self.refresh_weights()
         self.reset()
@@ -105,6 +108,7 @@ class StreamingSeparator:
     def reset(self):
         self.samples = None          # [M, s] pending input samples
         self.rings = None            # per block [M, R, H]
+        self._mkey = None
         self.tail = None             # [M, C, stride] pending overlap-add samples
         self.frames = 0              # frames emitted so far (= pos of the next frame)
 
@@ -126,12 +130,42 @@ class StreamingSeparator:
             self.rings.append(torch.zeros(M, R, self.H, device=dev))
         self.tail = torch.zeros(M, self.model.C, self.stride, device=dev)
 
+    def _model_struct(self):
+        """ctn_stream_model for ctn_stream_call (ABI v7): pointers into the snapshot and
+        the rings, rebuilt when either changes."""
+        key = (id(self.rings),)
+        if getattr(self, "_mkey", None) != key:
+            blocks = (L.StreamBlockParams * max(1, len(self.blocks)))()
+            for i, (b, ring) in enumerate(zip(self.blocks, self.rings)):
+                blocks[i] = L.StreamBlockParams(b["dil"], ring.shape[1],
+                                                *(b[k].data_ptr() for k in ("w1_t", "alpha1", "n1a", "n1b", "wd",
+                                                                            "alpha2", "n2a", "n2b", "w2_t")),
+                                                ring.data_ptr())
+            self._mblocks = blocks   # keeps the host array alive
+            self._mstruct = L.StreamModel(self.U.data_ptr(), self.g0.data_ptr(), self.b0.data_ptr(),
+                                          self.wb_t.data_ptr(), self.wm_t.data_ptr(), self.V.data_ptr(),
+                                          ctypes.cast(blocks, ctypes.c_void_p), len(self.blocks))
+            self._mkey = key
+        return self._mstruct
+
     def _call(self, buf: torch.Tensor, K: int) -> torch.Tensor:
-        """K frames whose samples start at buf[:, 0] -> [M, C, K*stride] finished samples."""
+        """K frames whose samples start at buf[:, 0] -> [M, C, K*stride] finished samples:
+        one ctn_stream_call (ABI v7: the whole network, 1x1 convs split over column chunks)."""
         m, lib = self.model, self.lib
         M, dev = buf.shape[0], buf.device
         d = self._desc(M, K)
         st = L.stream_handle(dev)
+        if self.one_call:
+            nb = lib.ctn_stream_workspace_bytes(ctypes.byref(d))
+            ws = L.workspace(nb, dev)
+            out = torch.empty(M, m.C, K * self.stride, device=dev)
+            tail = torch.empty_like(self.tail)
+            L.check(lib.ctn_stream_call(ctypes.byref(d), ctypes.byref(self._model_struct()), self.frames,
+                                        buf.data_ptr(), buf.stride(0), self.tail.data_ptr(), tail.data_ptr(),
+                                        out.data_ptr(), ws.data_ptr(), nb, st), "ctn_stream_call")
+            self.tail = tail
+            self.frames += K
+            return out
         w = torch.empty(M, K, m.N, device=dev)
         x = torch.empty(M, K, self.B, device=dev)
         L.check(lib.ctn_stream_encode(ctypes.byref(d), buf.data_ptr(), buf.stride(0), self.U.data_ptr(),

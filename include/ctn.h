@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define CTN_ABI_VERSION 6
+#define CTN_ABI_VERSION 7
 
 typedef enum { CTN_DTYPE_F32 = 0, CTN_DTYPE_BF16 = 1 } ctn_dtype;
 /* CTN_NORM_BN: torch.nn.BatchNorm1d, chose_norm's fallback branch (conv_tasnet.py:302-303) */
@@ -322,6 +322,42 @@ int ctn_stream_block(const ctn_stream_desc* d, int dilation, int64_t pos, int ri
 int ctn_stream_decode(const ctn_stream_desc* d, const float* x_last, const float* w, const float* wm_t,
                       const float* V, const float* tail_in, float* tail_out, float* frames_ws, float* out,
                       void* stream);
+
+/* ABI v7: one whole call (encode, every TemporalBlock, decode) in one entry, its 1x1
+ * convs split over 32-output column chunks so that a call with few new frames spreads
+ * over many CUs (the v5 entries give each (stream, 8 frames) one workgroup that streams
+ * every 1x1 weight through one CU).  Same state and layouts as the v5 entries; `blocks`
+ * is a HOST array of nblocks per-block parameter sets (separator order), each with its
+ * own ring.  `pos` as above; `tail_in` / `tail_out` [M][C][L/2] must not alias.
+ * `ws` >= ctn_stream_workspace_bytes(d).  Same arithmetic as the v5 path (the 1x1 sums
+ * are added in another order: results agree to fp32 rounding). */
+typedef struct {
+  int32_t dilation, ring_frames;
+  const float* w1_t;     /* [B][H] */
+  const float* alpha1;
+  const float* norm1_a;
+  const float* norm1_b;
+  const float* wd;       /* [H][P] */
+  const float* alpha2;
+  const float* norm2_a;
+  const float* norm2_b;
+  const float* w2_t;     /* [H][B] */
+  float* ring;           /* [M][ring_frames][H] */
+} ctn_stream_block_params;
+typedef struct {
+  const float* U;        /* [N][L] */
+  const float* gamma0;   /* separator cLN */
+  const float* beta0;
+  const float* wb_t;     /* [N][B] */
+  const float* wm_t;     /* [B][C*N] */
+  const float* V;        /* [L][N] */
+  const ctn_stream_block_params* blocks;
+  int32_t nblocks;
+} ctn_stream_model;
+size_t ctn_stream_workspace_bytes(const ctn_stream_desc* d);
+int ctn_stream_call(const ctn_stream_desc* d, const ctn_stream_model* model, int64_t pos, const float* samples,
+                    int64_t ld_samples, const float* tail_in, float* tail_out, float* out, void* ws,
+                    size_t ws_bytes, void* stream);
 
 /* -------------------------------------------------------------------------
  * Opt-in kernel timer (bench.py roofline): when enabled, every launch of the

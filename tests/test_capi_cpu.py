@@ -119,3 +119,33 @@ def test_pack_weights_validation(lib):
     assert "multiples of 32" in lib.ctn_last_error().decode()
     ragged_t = (L.WeightPack * 1)(L.WeightPack(16, 64, 72, None, None, None, 256))
     assert lib.ctn_pack_weights(ragged_t, 1, None) == 1
+
+
+def test_device_code_has_no_packed_fp32(tmp_path):
+    """The library's gfx950 code objects contain no packed-FP32 VALU instructions
+    (v_pk_fma/mul/add_f32): on gfx950 a packed instruction that takes a source half through
+    op_sel/op_sel_hi right after the VALU that wrote that register occasionally reads the
+    stale value when another wave on the SIMD is busy, and the compiler inserts no wait
+    state for it (tools/microbench/pk_hazard.hip).  The Makefile builds with
+    the packed-fp32-ops target feature off; this guards against a build without it."""
+    import re
+    import shutil
+    import subprocess
+    objdump = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    if not os.path.exists(objdump):
+        pytest.skip("llvm-objdump not available")
+    lib = os.path.join(ROOT, "conv-tasnet_amd", "libctn_hip.so")
+    if not os.path.exists(lib):
+        pytest.skip("libctn_hip.so not built")
+    shutil.copy(lib, tmp_path / "lib.so")
+    subprocess.run([objdump, "--offloading", "lib.so"], cwd=tmp_path, check=True, capture_output=True)
+    objs = [p for p in os.listdir(tmp_path) if "gfx950" in p]
+    assert objs, "no gfx950 code object in the library"
+    pk = re.compile(r"\bv_pk_(fma|mul|add)_f32\b")
+    n_pk = n_mfma = 0
+    for o in objs:
+        txt = subprocess.run([objdump, "-d", o], cwd=tmp_path, check=True, capture_output=True, text=True).stdout
+        n_pk += len(pk.findall(txt))
+        n_mfma += txt.count("v_mfma_")
+    assert n_mfma > 0, "disassembly found no MFMA: the check itself is broken"
+    assert n_pk == 0, f"{n_pk} packed-FP32 instructions in the device code"

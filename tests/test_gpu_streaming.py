@@ -130,3 +130,25 @@ def test_stream_push_after_flush_starts_a_new_stream():
     assert torch.equal(first, second)
     with pytest.raises(ValueError):
         streaming.StreamingSeparator(m, act_dtype=torch.bfloat16)
+
+
+@pytest.mark.parametrize("norm,mask,C", [("cLN", "relu", 2), ("BN", "softmax", 3)])
+def test_stream_one_call_matches_stage_entries(norm, mask, C):
+    """ctn_stream_call (ABI v7: the whole call in one entry, 1x1 convs split over 32-output
+    column chunks, per-frame norms recomputed by every chunk) against the v5 per-stage
+    entries on the same chunks: the same arithmetic with the 1x1 sums added in another
+    order, so the outputs agree to fp32 rounding, and the carried state stays in step."""
+    import streaming
+    m = _model(norm=norm, mask=mask, C=C)
+    if norm == "BN":
+        m.eval()
+    mix = torch.randn(2, 3000, device=DEV)
+    outs = []
+    for one in (True, False):
+        s = streaming.StreamingSeparator(m, max_frames=7)
+        s.one_call = one
+        parts = [s.push(mix[:, i:i + 333]) for i in range(0, 3000, 333)]
+        parts.append(s.flush())
+        outs.append(torch.cat(parts, dim=2))
+    assert outs[0].shape == outs[1].shape
+    assert rel(outs[0], outs[1]) < 1e-5, rel(outs[0], outs[1])
