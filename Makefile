@@ -59,10 +59,19 @@ build/dual_ws_bench_%: tools/microbench/dual_ws_bench.hip $(PKG)/csrc/ctn_dual_w
 .PHONY: dualws
 
 # diagnostic builds of the wave-specialised kernel: build/dual_ws_dbg_<bits>
-DV_DBGS := 16 17 18 20 0 8
+DV_DBGS := 16 8
 dualwsdbg: $(patsubst %,build/dual_ws_dbg_%,$(DV_DBGS))
 build/dual_ws_dbg_%: tools/microbench/dual_ws_bench.hip $(PKG)/csrc/ctn_dual_ws.hip $(PKG)/csrc/ctn_gemm_dual.hip $(HDR)
 	@mkdir -p build
 	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -Iinclude $(DEVFLAGS) -DCTN_DV_DBG=$* $< -o $@
 
+# slot layout x ring depth: build/dual_ws_var_<rawb>_<nsl>_<exp> (CTN_DV_RAWB, CTN_DV_NSL, CTN_DV_EXP)
+DV_VARS := 0_4_0 0_4_1 1_4_0 1_5_0 1_6_0 1_4_1 1_6_1
+dualwsvar: $(patsubst %,build/dual_ws_var_%,$(DV_VARS))
+build/dual_ws_var_%: tools/microbench/dual_ws_bench.hip $(PKG)/csrc/ctn_dual_ws.hip $(PKG)/csrc/ctn_gemm_dual.hip $(HDR)
+	@mkdir -p build
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -Iinclude $(DEVFLAGS) -DCTN_DV_RAWB=$(word 1,$(subst _, ,$*)) \
+	  -DCTN_DV_NSL=$(word 2,$(subst _, ,$*)) -DCTN_DV_EXP=$(word 3,$(subst _, ,$*)) $< -o $@
+
+.PHONY: dualwsvar
 .PHONY: dualwsdbg

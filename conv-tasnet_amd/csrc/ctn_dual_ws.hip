@@ -10,22 +10,23 @@
 //
 // Schedule.  gemm_dual_kernel runs every wave through one barrier per tile: wait for
 // the tile's LDS-DMA, then staging, MFMA and epilogue in lockstep, so the phases add
-// up.  Here the roles are split inside the workgroup (12 waves,
-// 3 per SIMD):
-//   * 4 memory waves load the tiles into registers PF tiles ahead (plain global
-//     loads, no LDS-DMA), apply the column operand's PReLU + norm on the way, write
-//     the tile's images (A = gy in MFMA fragment order, B = op(d), R = raw d, row
-//     statistics) into an LDS ring of NSL slots, publish FULL, and store the C image
-//     consumers left in the slot NSL tiles earlier (whole 16-byte lanes, full rows);
-//   * 8 consumer waves wait for FULL, run the row GEMM (resident W2 fragments, both
-//     16-row blocks of the tile), the column GEMM (dW2 slice as MFMA accumulators),
-//     the norm-2 backward epilogue into the slot's C image, and publish DONE.
-// FULL / DONE are one generation word per wave per slot in LDS (the memory waves wait
-// for the consumers' DONE of tile t-NSL before refilling its slot), so the MFMAs of
-// one tile overlap the loads, transforms and stores of the next ones, and no wave
-// ever waits on another wave's memory operations.  Every LDS read of another wave's
-// data happens after that wave's `s_waitcnt lgkmcnt(0)` + generation-word store and
-// this wave's matching generation-word load.
+// up.  Here the roles are split inside the workgroup (16 waves,
+// 4 per SIMD):
+//   * 4 memory waves LDS-DMA the tiles PF tiles ahead into an LDS ring of NSL slots
+//     (A = gy in MFMA fragment order, R = raw d of the slice, the tile's statistics),
+//     wait for their own DMA with a counted vmcnt, write B = op(d) (PReLU + norm + affine,
+//     bf16) from R, and publish FULL;
+//   * 4 row waves (32 output channels each, resident W2 fragments) run the row GEMM of
+//     both 16-row blocks and the norm-2 backward epilogue (hat a from R in fp32), store
+//     C straight to memory and publish DONE;
+//   * 8 column waves accumulate the dW2 slice (64 x 64 each) as MFMA accumulators from
+//     A and B and publish DONE.
+// FULL / DONE are one generation word per wave per slot in LDS (a memory wave waits
+// for every DONE of tile t-NSL before refilling its slot), so the MFMAs of one tile
+// overlap the DMA and transforms of the next ones, and no wave ever waits on another
+// wave's memory operations.  Every LDS read of another wave's data happens after that
+// wave's `s_waitcnt lgkmcnt(0)` + generation-word store and this wave's matching
+// generation-word load.
 #include <stdlib.h>
 
 #include "ctn_common.h"
@@ -46,7 +47,20 @@ constexpr int DV_NT = (DV_ND + DV_NMW) * 64;     // 1024 threads
 constexpr int DV_KB = 8, DV_KR = 256;            // reduction of the row part (gy channels)
 constexpr int DV_NS = 128;                       // output channels per slice
 constexpr int DV_GRID = 256;
-constexpr int DV_NSL = 4;                        // LDS ring slots (NSL - 1 tiles in flight)
+// Slot layout.  CTN_DV_RAWB=1 (default): the B image holds the raw d slice exactly as the
+// LDS-DMA lands it (row-major, 16-byte granules swizzled per row); the column waves apply
+// PReLU + norm + affine to their B fragments, the row waves read raw d from it, and no
+// other image exists, so a slot is 24.8 KB and the ring holds 6 tiles.  CTN_DV_RAWB=0:
+// the memory waves write op(d) into a separate B image from a raw-d image R (33 KB slots,
+// ring of 4).
+#ifndef CTN_DV_RAWB
+#define CTN_DV_RAWB 1
+#endif
+constexpr bool DV_RB = CTN_DV_RAWB;
+#ifndef CTN_DV_NSL
+#define CTN_DV_NSL (CTN_DV_RAWB ? 6 : 4)
+#endif
+constexpr int DV_NSL = CTN_DV_NSL;               // LDS ring slots (NSL - 1 tiles in flight)
 
 // Bound-finding builds only (tools/microbench/dual_bench.hip -DCTN_DV_EXP=<bits>):
 // bit 0 consumers skip all arithmetic (wait FULL, publish DONE), bit 1 no column part,
@@ -54,20 +68,20 @@ constexpr int DV_NSL = 4;                        // LDS ring slots (NSL - 1 tile
 #ifndef CTN_DV_EXP
 #define CTN_DV_EXP 0
 #endif
-// Diagnostic builds (tools/microbench/dual_ws_bench.hip): bit 0 lgkmcnt(0) after the
-// memory waves' R-image writes, bit 1 R image written after the B image, bit 2
-// lgkmcnt(0) after the consumers' C-image writes, bit 4 consumers store the raw d
-// values they read from the R image in place of C (checked against d on the host).
+// Diagnostic builds (tools/microbench/dual_ws_bench.hip): bit 4 the row waves store the
+// raw d values they read from the ring in place of C (checked against d on the host);
+// bit 3 is the bench's own (per-launch statistics dump).
 #ifndef CTN_DV_DBG
 #define CTN_DV_DBG 0
 #endif
 
 // slot layout (bytes)
 constexpr int DV_A = DV_TM * DV_KR * 2;          // 16384: gy tile, WS fragment image (du_apiece)
-constexpr int DV_BST = 1024 + 32;                // B image block stride: 16 columns x 32 rows + 32 B
-constexpr int DV_B = 8 * DV_BST;                 // op(d) slice in 4-row x 16-column blocks (du_boff)
-constexpr int DV_R = DV_TM * DV_NS * 2;          // 8192: raw d rows, 16-byte granules XOR row
-constexpr int DV_ST = DV_NMW * 256;              // statistics: 256 B per memory wave
+constexpr int DV_BST = 1024 + 32;                // (RAWB=0) B block stride: 16 columns x 32 rows + 32 B
+constexpr int DV_B = DV_RB ? DV_TM * DV_NS * 2   // raw d slice, 256-byte rows (dv_rbgr)
+                           : 8 * DV_BST;         // op(d) slice in 4-row x 16-column blocks (du_boff)
+constexpr int DV_R = DV_RB ? 0 : DV_TM * DV_NS * 2;   // (RAWB=0) raw d rows, 16-byte granules XOR row
+constexpr int DV_ST = DV_RB ? 256 : DV_NMW * 256;     // statistics (RAWB=0: 256 B per memory wave)
 constexpr int OFF_A = 0, OFF_B = OFF_A + DV_A, OFF_R = OFF_B + DV_B, OFF_ST = OFF_R + DV_R;
 constexpr int DV_SLOT = OFF_ST + DV_ST;
 
@@ -81,8 +95,30 @@ CTN_DEV int dv_boff(int row, int col) {
   const int rg = row >> 2;
   return ((rg ^ ((rg >> 1) & 1)) << 7) + (row & 3) * 32 + (col & 15) * 2;
 }
-// 16-byte granule g (channels 8g..8g+7) of row r in the R / C images
+// 16-byte granule g (channels 8g..8g+7) of row r in the R image (RAWB=0)
 CTN_DEV int dv_roff(int r, int g) { return r * 256 + ((g ^ (r & 15)) << 4); }
+// RAWB=1 B image: granule g of row r at r * 256 + 16 * position, position = g's low bit
+// and (g/2) XOR a 3-bit row hash.  The hash differs between the 8 rows a column wave's
+// transposed 8-byte reads touch in one half-wave ({q, 8+q} or {4+q, 12+q}, q < 4, and the
+// same + 16), so those 32 reads hit 32 distinct 8-byte bank pairs; a row wave's 16-byte
+// reads of 16 rows see at most 2-way conflicts.
+CTN_DEV int dv_rbhash(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
+CTN_DEV int dv_rbpos(int r, int g) { return (g & 1) | ((((g >> 1) ^ dv_rbhash(r)) & 7) << 1); }
+CTN_DEV int dv_rbgr(int r, int g) { return r * 256 + (dv_rbpos(r, g) << 4); }
+// counted wait for the RAWB=1 ring depth (up to 5 tiles x 7 DMA instructions in flight)
+CTN_DEV void dv_vmwait(int n) {
+#define CTN_VMW(k) \
+  case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+  switch (n < 0 ? 0 : n) {
+    CTN_VMW(0) CTN_VMW(1) CTN_VMW(2) CTN_VMW(3) CTN_VMW(4) CTN_VMW(5) CTN_VMW(6) CTN_VMW(7)
+    CTN_VMW(8) CTN_VMW(9) CTN_VMW(10) CTN_VMW(11) CTN_VMW(12) CTN_VMW(13) CTN_VMW(14) CTN_VMW(15)
+    CTN_VMW(16) CTN_VMW(17) CTN_VMW(18) CTN_VMW(19) CTN_VMW(20) CTN_VMW(21) CTN_VMW(22) CTN_VMW(23)
+    CTN_VMW(24) CTN_VMW(25) CTN_VMW(26) CTN_VMW(27) CTN_VMW(28) CTN_VMW(29) CTN_VMW(30) CTN_VMW(31)
+    CTN_VMW(32) CTN_VMW(33) CTN_VMW(34)
+    default: asm volatile("s_waitcnt vmcnt(35)" ::: "memory"); break;
+  }
+#undef CTN_VMW
+}
 
 CTN_DEV s16x4_t dv_tr(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(p));
@@ -183,7 +219,8 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
     *reinterpret_cast<float4*>(gam) = *reinterpret_cast<const float4*>(p.gamma + n0 + cl);
     *reinterpret_cast<float4*>(gam + 4) = *reinterpret_cast<const float4*>(p.gamma + n0 + cl + 4);
     const int rbase = lg * 256 + ((lr ^ ((lg & 1) * 12)) << 4);   // + rb * KB * 1024 + kb * 1024
-    const int ro = dv_roff(lr, 4 * r + lg);                        // row lr; row 16 + lr at + 4096
+    const int ro = DV_RB ? OFF_B + dv_rbgr(lr, 4 * r + lg)          // row lr; row 16 + lr at + 4096
+                         : OFF_R + dv_roff(lr, 4 * r + lg);
 
     double run_s = 0.0, run_q = 0.0;
     const int m0 = t0 / tpu;
@@ -220,9 +257,10 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
           float s1[2] = {0.f, 0.f}, q1[2] = {0.f, 0.f};
 #pragma unroll
           for (int rb = 0; rb < 2; ++rb) {
-            const v4u rw = *reinterpret_cast<const v4u*>(base + OFF_R + ro + rb * 4096);
+            const v4u rw = *reinterpret_cast<const v4u*>(base + ro + rb * 4096);
             float2 est;
             if constexpr (NK == NORM_GLN) est = *reinterpret_cast<const float2*>(base + OFF_ST);   // the tile's utterance
+            else if constexpr (DV_RB) est = *reinterpret_cast<const float2*>(base + OFF_ST + (16 * rb + lr) * 8);
             else est = *reinterpret_cast<const float2*>(base + OFF_ST + (2 * rb + (lr >> 3)) * 256 + (lr & 7) * 8);
             const float rs = est.y, ms = -est.x * est.y;
             const bool ok = NK == NORM_GLN || (t * TM) % Kp + 16 * rb + lr < Kv;   // cLN padded frames: stats not finite
@@ -288,7 +326,8 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) dacc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    // lane-constant LDS addresses (ctn_gemm_dual.hip's, B blocks at stride DV_BST)
+    // lane-constant LDS addresses (ctn_gemm_dual.hip's A addressing; B: RAWB=1 row-major
+    // granules, block j at bbase ^ (j << 5); RAWB=0 blocks at stride DV_BST)
     const int q = lr >> 2, pp = lr & 3;
     int abase[2], bbase[2];
 #pragma unroll
@@ -296,37 +335,86 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
       const int row = 8 * lg + 4 * h + q;
       abase[h] = (lg >> 1) * KB * 1024 + 2 * wp * 1024 + (pp >> 1) * 256 + (((row & 15) ^ ((pp >> 1) * 12)) << 4) +
                  (pp & 1) * 8;
-      bbase[h] = wn * 4 * DV_BST + dv_boff(row, 4 * pp);
+      bbase[h] = DV_RB ? dv_rbgr(row, 8 * wn + (pp >> 1)) + 8 * (pp & 1) : wn * 4 * DV_BST + dv_boff(row, 4 * pp);
     }
-    int slot = 0;
-    uint32_t gen = 1;
-    for (int t = t0; t < t1; ++t) {
-      dv_wait<4>(fl_full[slot], gen);
-      const char* base = smem + slot * SLOT;
-      if constexpr (!(CTN_DV_EXP & 3)) {
-        const char* a = base + OFF_A;
-        const char* bb = base + OFF_B;
-        bf16x8_t bfr[4];
+    // RAWB=1: the B fragment of block j holds raw d of column 16 (4 wn + j) + lr (slice-local)
+    // at frame rows 8 lg .. 8 lg + 7; op(d) is applied here with the memory-side transform's
+    // exact float operations (so C, Dpart and the statistics match RAWB=0 bit for bit)
+    float cg[4], cb[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const s16x4_t lo = dv_tr(bb + bbase[0] + j * DV_BST), hi = dv_tr(bb + bbase[1] + j * DV_BST);
-          bfr[j] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    for (int j = 0; j < 4; ++j) {
+      cg[j] = sgb[0][16 * (4 * wn + j) + lr];
+      cb[j] = sgb[1][16 * (4 * wn + j) + lr];
+    }
+    const float bal = p.bop.alpha[0];
+    auto run = [&](auto le1) __attribute__((always_inline)) {
+      constexpr bool LE1 = decltype(le1)::value;
+      int slot = 0;
+      uint32_t gen = 1;
+      for (int t = t0; t < t1; ++t) {
+        dv_wait<4>(fl_full[slot], gen);
+        const char* base = smem + slot * SLOT;
+        if constexpr (!(CTN_DV_EXP & 3)) {
+          const char* a = base + OFF_A;
+          const char* bb = base + OFF_B;
+          bf16x8_t bfr[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const s16x4_t lo = dv_tr(bb + (DV_RB ? bbase[0] ^ (j << 5) : bbase[0] + j * DV_BST));
+            const s16x4_t hi = dv_tr(bb + (DV_RB ? bbase[1] ^ (j << 5) : bbase[1] + j * DV_BST));
+            bfr[j] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          }
+          if constexpr (DV_RB) {
+            float mu[8], rs[8];
+            if constexpr (NK == NORM_GLN) {
+              const float2 st = *reinterpret_cast<const float2*>(base + OFF_ST);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) mu[e] = st.x, rs[e] = st.y;
+            } else {
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                const float4 st = *reinterpret_cast<const float4*>(base + OFF_ST + 64 * lg + 16 * k);
+                mu[2 * k] = st.x, rs[2 * k] = st.y, mu[2 * k + 1] = st.z, rs[2 * k + 1] = st.w;
+              }
+            }
+            const int tk = (t * TM) % Kp;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              v4u v = __builtin_bit_cast(v4u, bfr[j]);
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                float x0 = __uint_as_float(v[k] << 16), x1 = __uint_as_float(v[k] & 0xffff0000u);
+                x0 = LE1 ? fmaxf(x0, x0 * bal) : fminf(x0, x0 * bal);   // PReLU
+                x1 = LE1 ? fmaxf(x1, x1 * bal) : fminf(x1, x1 * bal);
+                x0 = fmaf(x0 - mu[2 * k], rs[2 * k] * cg[j], cb[j]);
+                x1 = fmaf(x1 - mu[2 * k + 1], rs[2 * k + 1] * cg[j], cb[j]);
+                if constexpr (NK == NORM_CLN) {   // padded frames: statistics not finite
+                  if (tk + 8 * lg + 2 * k >= Kv) x0 = 0.f;
+                  if (tk + 8 * lg + 2 * k + 1 >= Kv) x1 = 0.f;
+                }
+                v[k] = pk_bf16(x0, x1);
+              }
+              bfr[j] = __builtin_bit_cast(bf16x8_t, v);
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int o = (i >> 1) * 1024 + (i & 1) * 512;
+            const s16x4_t lo = dv_tr(a + abase[0] + o), hi = dv_tr(a + abase[1] + o);
+            const bf16x8_t af = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) dacc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], dacc[i][j], 0, 0, 0);
+          }
         }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int o = (i >> 1) * 1024 + (i & 1) * 512;
-          const s16x4_t lo = dv_tr(a + abase[0] + o), hi = dv_tr(a + abase[1] + o);
-          const bf16x8_t af = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-#pragma unroll
-          for (int j = 0; j < 4; ++j) dacc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], dacc[i][j], 0, 0, 0);
+        dv_signal(&fl_done[slot][DV_NR + c], gen);
+        if (++slot == NSL) {
+          slot = 0;
+          ++gen;
         }
       }
-      dv_signal(&fl_done[slot][DV_NR + c], gen);
-      if (++slot == NSL) {
-        slot = 0;
-        ++gen;
-      }
-    }
+    };
+    if (bal <= 1.f) run(std::true_type{});
+    else run(std::false_type{});
     // dW2 partial of this workgroup: lane holds D[(wp*4+i)*16 + 4lg + e][n0 + (wn*4+j)*16 + lr]
     float* Dp = p.Dpart + (size_t)rr * KR * p.Nout;
 #pragma unroll
@@ -345,9 +433,10 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
   // raw-d pieces 2m, 2m+1 (4 rows x the slice's 128 channels each) and its statistics
   // piece by LDS-DMA (buffer_load ... lds: no registers, PF tiles ahead), waits for its
   // own DMA group with a counted vmcnt (no other memory operations are issued by these
-  // waves), reads back its own raw-d pieces to write op(d) into the B image, and
-  // publishes FULL.  A slot is refilled only after every row / column wave's DONE for the
-  // tile that used it last.
+  // waves), (RAWB=0 only) reads back its own raw-d pieces to write op(d) into the B image,
+  // and publishes FULL.  A slot is refilled only after every row / column wave's DONE for
+  // the tile that used it last.  RAWB=1: the raw-d pieces land in the B image itself and
+  // wave 0 alone fetches the tile's statistics (all 32 rows).
   const int mw = wid - DV_ND;
   const rsrc_t rA = du_rsrc(p.A, rows * p.lda * 2), rD = du_rsrc(p.Bm, rows * p.ldb * 2);
   const rsrc_t rS = du_rsrc(p.bop.stats, (NK == NORM_GLN ? (long)p.g.M : rows) * 8);
@@ -360,23 +449,27 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
     aoff[u] = (uint32_t)(arow[u] * p.lda + (4 * kb + (lane >> 4)) * 8) * 2u;
   }
   // raw-d piece i = 2*mw + h: row 4i + L/16, granule position L%16 holds channels
-  // 8g .. 8g+7, g = (L%16) ^ (row%16) (the R image's swizzle, applied on the source)
+  // 8g .. 8g+7 with g = (L%16) ^ (row%16) (RAWB=0: the R image's swizzle) or g the granule
+  // at B position L%16 (RAWB=1: dv_rbpos inverted), the swizzle applied on the source
   int drow[2], dgr[2], boff[2];
   uint32_t doff[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     drow[h] = 4 * (2 * mw + h) + (lane >> 4);
-    dgr[h] = (lane & 15) ^ (drow[h] & 15);
+    const int ps = lane & 15;
+    dgr[h] = DV_RB ? (ps & 1) | ((((ps >> 1) ^ dv_rbhash(drow[h])) & 7) << 1) : ps ^ (drow[h] & 15);
     doff[h] = (uint32_t)(drow[h] * p.ldb + n0 + 8 * dgr[h]) * 2u;
     boff[h] = (dgr[h] >> 1) * DV_BST + dv_boff(drow[h], 8 * (dgr[h] & 1));
   }
-  // statistics piece: cLN rows 8m .. 8m+7 (lanes 0..15, one dword each); gLN the tile's
-  // utterance pair (wave 0, lanes 0..1); other lanes read out of range (zeros) into the
-  // wave's own 256 bytes
-  const bool st_lane = NK == NORM_CLN ? lane < 16 : (mw == 0 && lane < 2);
-  const uint32_t soff = st_lane ? (uint32_t)((NK == NORM_CLN ? 8 * mw * 8 : 0) + lane * 4) : DU_OOB;
+  // statistics: RAWB=1 wave 0 fetches the tile's (cLN: 32 rows, one dword per lane; gLN:
+  // the utterance pair, lanes 0..1).  RAWB=0 every wave fetches into its own 256 bytes (a
+  // wave's vmcnt covers only its own DMA, and each reads statistics it fetched itself):
+  // cLN rows 8m .. 8m+7 (lanes 0..15), gLN the pair.  Other lanes read out of range (zeros).
+  const bool st_lane = NK == NORM_CLN ? (DV_RB ? true : lane < 16) : lane < 2;
+  const uint32_t soff = st_lane ? (uint32_t)((NK == NORM_CLN && !DV_RB ? 8 * mw * 8 : 0) + lane * 4) : DU_OOB;
+  const bool st_wave = !DV_RB || mw == 0;
   const float bal = p.bop.alpha[0];
-  constexpr int G = 7;   // DMA instructions per wave and tile
+  const int G = st_wave ? 7 : 6;   // DMA instructions per wave and tile
 
   auto dma = [&](int t) __attribute__((always_inline)) {
     char* base = smem + ((t - t0) % NSL) * SLOT;
@@ -385,8 +478,8 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
     for (int u = 0; u < 4; ++u)   // rows of padded frames arrive as zeros (out-of-range offset)
       du_dma16(rA, base + OFF_A + (4 * mw + u) * 1024, tk + arow[u] < Kv ? aoff[u] : DU_OOB, t * TM * p.lda * 2);
 #pragma unroll
-    for (int h = 0; h < 2; ++h) du_dma16(rD, base + OFF_R + (2 * mw + h) * 1024, doff[h], t * TM * p.ldb * 2);
-    du_dma4(rS, base + OFF_ST + mw * 256, soff, NK == NORM_GLN ? (t / tpu) * 8 : t * TM * 8);
+    for (int h = 0; h < 2; ++h) du_dma16(rD, base + (DV_RB ? OFF_B : OFF_R) + (2 * mw + h) * 1024, doff[h], t * TM * p.ldb * 2);
+    if (st_wave) du_dma4(rS, base + OFF_ST + (DV_RB ? 0 : mw * 256), soff, NK == NORM_GLN ? (t / tpu) * 8 : t * TM * 8);
   };
   auto transform = [&](auto le1, int t, char* base) __attribute__((always_inline)) {
     constexpr bool LE1 = decltype(le1)::value;
@@ -395,7 +488,7 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
     for (int h = 0; h < 2; ++h) {
       const int row = drow[h];
       v4u v = *reinterpret_cast<const v4u*>(base + OFF_R + (2 * mw + h) * 1024 + lane * 16);
-      const float2 st = *reinterpret_cast<const float2*>(base + OFF_ST + (NK == NORM_GLN ? 0 : mw * 256 + (row & 7) * 8));
+      const float2 st = *reinterpret_cast<const float2*>(base + OFF_ST + mw * 256 + (NK == NORM_GLN ? 0 : (row & 7) * 8));
       float gam[8], bet[8];
       *reinterpret_cast<float4*>(gam) = *reinterpret_cast<const float4*>(&sgb[0][8 * dgr[h]]);
       *reinterpret_cast<float4*>(gam + 4) = *reinterpret_cast<const float4*>(&sgb[0][8 * dgr[h] + 4]);
@@ -422,9 +515,13 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
     uint32_t gen = 1;
     for (int t = t0; t < t1; ++t) {
       const int later = t1 - 1 - t < PF - 1 ? t1 - 1 - t : PF - 1;   // DMA groups issued after tile t's
-      vmwait23(G * later);
       char* base = smem + slot * SLOT;
-      transform(le1, t, base);
+      if constexpr (DV_RB) {
+        dv_vmwait(G * later);
+      } else {
+        vmwait23(G * later);
+        transform(le1, t, base);
+      }
       dv_signal(&fl_full[slot][mw], gen);
       const int tn = t + PF;
       if (tn < t1) {
