@@ -65,13 +65,14 @@ build/dual_ws_dbg_%: tools/microbench/dual_ws_bench.hip $(PKG)/csrc/ctn_dual_ws.
 	@mkdir -p build
 	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -Iinclude $(DEVFLAGS) -DCTN_DV_DBG=$* $< -o $@
 
-# slot layout x ring depth: build/dual_ws_var_<rawb>_<nsl>_<exp> (CTN_DV_RAWB, CTN_DV_NSL, CTN_DV_EXP)
-DV_VARS := 0_4_0 0_4_1 1_4_0 1_5_0 1_6_0 1_4_1 1_6_1
+# slot layout x ring depth x column split: build/dual_ws_var_<rawb>_<nsl>_<cj>_<exp>
+# (CTN_DV_RAWB, CTN_DV_NSL, CTN_DV_CJ, CTN_DV_EXP)
+DV_VARS := 0_4_4_0 0_4_2_0 0_4_1_0 1_6_4_0 1_6_2_0 1_6_1_0 0_4_2_2 1_6_2_2 0_4_2_8 1_6_2_8 0_4_2_18 1_6_2_18 1_6_2_10 0_4_2_10
 dualwsvar: $(patsubst %,build/dual_ws_var_%,$(DV_VARS))
 build/dual_ws_var_%: tools/microbench/dual_ws_bench.hip $(PKG)/csrc/ctn_dual_ws.hip $(PKG)/csrc/ctn_gemm_dual.hip $(HDR)
 	@mkdir -p build
 	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -Iinclude $(DEVFLAGS) -DCTN_DV_RAWB=$(word 1,$(subst _, ,$*)) \
-	  -DCTN_DV_NSL=$(word 2,$(subst _, ,$*)) -DCTN_DV_EXP=$(word 3,$(subst _, ,$*)) $< -o $@
+	  -DCTN_DV_NSL=$(word 2,$(subst _, ,$*)) -DCTN_DV_CJ=$(word 3,$(subst _, ,$*)) -DCTN_DV_EXP=$(word 4,$(subst _, ,$*)) $< -o $@
 
 .PHONY: dualwsvar
 .PHONY: dualwsdbg

@@ -1643,11 +1643,46 @@ extern "C" int ctn_stream_decode(const ctn_stream_desc* d, const float* x_last, 
 }
 
 // ABI v7: one whole streaming call (ctn_stream.hip, launch_stream_call_stage)
+namespace {
+size_t stream_ws_floats(const ctn_stream_desc* d) {
+  const size_t M = d->M, K = d->K;
+  return M * K * d->N + 2 * M * K * d->B + M * K * (size_t)(d->H > d->C * d->N ? d->H : d->C * d->N);
+}
+// the replayed graph's pos slot: 16-byte aligned, inside the workspace's 256-byte tail
+long* stream_pos_slot(const ctn_stream_desc* d, void* ws) {
+  const size_t off = (stream_ws_floats(d) * sizeof(float) + 15) / 16 * 16;
+  return reinterpret_cast<long*>(reinterpret_cast<char*>(ws) + off);
+}
+// CTN_STREAM_GRAPH=0: launch the stages directly on every call (A/B only)
+bool stream_graph_enabled() {
+  const char* e = getenv("CTN_STREAM_GRAPH");
+  return e ? atoi(e) != 0 : true;
+}
+struct StreamGraph {
+  std::vector<uintptr_t> key;
+  hipGraphExec_t exec;
+};
+std::mutex g_sg_mu;
+std::vector<StreamGraph> g_sg;   // most recently stored last; at most 8
+hipGraphExec_t stream_graph_find(const std::vector<uintptr_t>& key) {
+  std::lock_guard<std::mutex> lk(g_sg_mu);
+  for (const StreamGraph& g : g_sg)
+    if (g.key == key) return g.exec;
+  return nullptr;
+}
+void stream_graph_store(const std::vector<uintptr_t>& key, hipGraphExec_t exec) {
+  std::lock_guard<std::mutex> lk(g_sg_mu);
+  if (g_sg.size() == 8) {
+    (void)hipGraphExecDestroy(g_sg.front().exec);
+    g_sg.erase(g_sg.begin());
+  }
+  g_sg.push_back(StreamGraph{key, exec});
+}
+}  // namespace
+
 extern "C" size_t ctn_stream_workspace_bytes(const ctn_stream_desc* d) {
   if (stream_check(d)) return 0;
-  const size_t M = d->M, K = d->K;
-  const size_t f = M * K * d->N + 2 * M * K * d->B + M * K * (size_t)(d->H > d->C * d->N ? d->H : d->C * d->N);
-  return f * sizeof(float) + 256;
+  return stream_ws_floats(d) * sizeof(float) + 256;
 }
 
 extern "C" int ctn_stream_call(const ctn_stream_desc* d, const ctn_stream_model* mdl, int64_t pos, const float* samples,
@@ -1673,33 +1708,83 @@ extern "C" int ctn_stream_call(const ctn_stream_desc* d, const ctn_stream_model*
       return fail(CTN_ERR_ARG, "block %d: null pointer", i);
   }
   const hipStream_t s = (hipStream_t)stream;
-  const size_t M = d->M, K = d->K;
-  float* w = reinterpret_cast<float*>(ws);
-  float* xa = w + M * K * d->N;
-  float* xb = xa + M * K * d->B;
-  float* scratch = xb + M * K * d->B;   // h1 of a block / the sources
-  StreamArgs a = stream_args(d);
-  a.pos = pos;
-  a.samples = samples; a.ld_samples = ld_samples; a.U = mdl->U; a.na = mdl->gamma0; a.nb = mdl->beta0;
-  a.W = mdl->wb_t; a.w_out = w; a.x_out = xa;
-  CTN_HIP(launch_stream_call_stage(0, a, s));
-  float* x = xa;
-  float* y = xb;
+  long* pos_dev = stream_pos_slot(d, ws);
+  // the launch sequence, parameterised by where `pos` comes from
+  auto enqueue = [&](hipStream_t q, const long* pd) -> hipError_t {
+    const size_t M = d->M, K = d->K;
+    float* w = reinterpret_cast<float*>(ws);
+    float* xa = w + M * K * d->N;
+    float* xb = xa + M * K * d->B;
+    float* scratch = xb + M * K * d->B;   // h1 of a block / the sources
+    StreamArgs a = stream_args(d);
+    a.pos = pos; a.pos_dev = pd;
+    a.samples = samples; a.ld_samples = ld_samples; a.U = mdl->U; a.na = mdl->gamma0; a.nb = mdl->beta0;
+    a.W = mdl->wb_t; a.w_out = w; a.x_out = xa;
+    hipError_t e = launch_stream_call_stage(0, a, q);
+    float* x = xa;
+    float* y = xb;
+    for (int i = 0; e == hipSuccess && i < mdl->nblocks; ++i) {
+      const ctn_stream_block_params& b = mdl->blocks[i];
+      StreamArgs ab = stream_args(d);
+      ab.pos = pos; ab.pos_dev = pd; ab.dil = b.dilation; ab.R = b.ring_frames; ab.ring = b.ring;
+      ab.x_in = x; ab.x_out = y; ab.frames = scratch;
+      ab.W = b.w1_t; ab.alpha1 = b.alpha1; ab.na = b.norm1_a; ab.nb = b.norm1_b;
+      ab.wd = b.wd; ab.alpha2 = b.alpha2; ab.na2 = b.norm2_a; ab.nb2 = b.norm2_b; ab.W2 = b.w2_t;
+      e = launch_stream_call_stage(1, ab, q);
+      if (e == hipSuccess) e = launch_stream_call_stage(2, ab, q);
+      float* t = x; x = y; y = t;
+    }
+    StreamArgs ad = stream_args(d);
+    ad.x_in = x; ad.w_in = w; ad.W = mdl->wm_t; ad.V = mdl->V; ad.frames = scratch;
+    ad.tail_in = tail_in; ad.tail_out = tail_out; ad.out = out;
+    if (e == hipSuccess) e = launch_stream_call_stage(3, ad, q);
+    if (e == hipSuccess) e = launch_stream_call_stage(4, ad, q);
+    return e;
+  };
+  if (!stream_graph_enabled()) {
+    CTN_HIP(enqueue(s, nullptr));
+    return CTN_OK;
+  }
+  // Graph replay: the 4 + 2 X R launches of a call are captured once per argument set
+  // (everything but pos, which the replay reads from the workspace) and replayed with
+  // one graph launch after a one-thread kernel stores pos.
+  std::vector<uintptr_t> key;
+  int dev = 0;
+  CTN_HIP(hipGetDevice(&dev));
+  key.push_back((uintptr_t)dev);
+  for (const int v : {d->M, d->K, d->N, d->L, d->B, d->H, d->P, d->C, d->norm, d->mask_type}) key.push_back((uintptr_t)(unsigned)v);
+  for (const void* v : {(const void*)mdl->U, (const void*)mdl->gamma0, (const void*)mdl->beta0, (const void*)mdl->wb_t,
+                        (const void*)mdl->wm_t, (const void*)mdl->V, (const void*)samples, (const void*)tail_in,
+                        (const void*)tail_out, (const void*)out, (const void*)ws})
+    key.push_back((uintptr_t)v);
+  key.push_back((uintptr_t)ld_samples);
   for (int i = 0; i < mdl->nblocks; ++i) {
     const ctn_stream_block_params& b = mdl->blocks[i];
-    StreamArgs ab = stream_args(d);
-    ab.pos = pos; ab.dil = b.dilation; ab.R = b.ring_frames; ab.ring = b.ring;
-    ab.x_in = x; ab.x_out = y; ab.frames = scratch;
-    ab.W = b.w1_t; ab.alpha1 = b.alpha1; ab.na = b.norm1_a; ab.nb = b.norm1_b;
-    ab.wd = b.wd; ab.alpha2 = b.alpha2; ab.na2 = b.norm2_a; ab.nb2 = b.norm2_b; ab.W2 = b.w2_t;
-    CTN_HIP(launch_stream_call_stage(1, ab, s));
-    CTN_HIP(launch_stream_call_stage(2, ab, s));
-    float* t = x; x = y; y = t;
+    key.push_back((uintptr_t)(unsigned)b.dilation);
+    key.push_back((uintptr_t)(unsigned)b.ring_frames);
+    for (const void* v : {(const void*)b.w1_t, (const void*)b.alpha1, (const void*)b.norm1_a, (const void*)b.norm1_b,
+                          (const void*)b.wd, (const void*)b.alpha2, (const void*)b.norm2_a, (const void*)b.norm2_b,
+                          (const void*)b.w2_t, (const void*)b.ring})
+      key.push_back((uintptr_t)v);
   }
-  StreamArgs ad = stream_args(d);
-  ad.x_in = x; ad.w_in = w; ad.W = mdl->wm_t; ad.V = mdl->V; ad.frames = scratch;
-  ad.tail_in = tail_in; ad.tail_out = tail_out; ad.out = out;
-  CTN_HIP(launch_stream_call_stage(3, ad, s));
-  CTN_HIP(launch_stream_call_stage(4, ad, s));
+  hipGraphExec_t exec = stream_graph_find(key);
+  if (!exec) {
+    hipStream_t cs = nullptr;
+    CTN_HIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    hipGraph_t g = nullptr;
+    hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
+    if (e == hipSuccess) {
+      const hipError_t el = enqueue(cs, pos_dev);
+      e = hipStreamEndCapture(cs, &g);
+      if (el != hipSuccess) e = el;
+    }
+    if (e == hipSuccess) e = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0);
+    if (g) (void)hipGraphDestroy(g);
+    (void)hipStreamDestroy(cs);
+    CTN_HIP(e);
+    stream_graph_store(key, exec);
+  }
+  CTN_HIP(launch_stream_set_pos(pos_dev, (long)pos, s));
+  CTN_HIP(hipGraphLaunch(exec, s));
   return CTN_OK;
 }

@@ -61,10 +61,19 @@ constexpr bool DV_RB = CTN_DV_RAWB;
 #define CTN_DV_NSL (CTN_DV_RAWB ? 6 : 4)
 #endif
 constexpr int DV_NSL = CTN_DV_NSL;               // LDS ring slots (NSL - 1 tiles in flight)
+// Column-wave split of the 256 x 128 dW2 slice: each of the 8 waves owns CJ 16-column
+// blocks x (16 / CJ) 16-row blocks (64 accumulator registers either way).  Fewer column
+// blocks per wave means fewer waves share (and, RAWB=1, transform) each B fragment, at
+// the price of more A fragment reads per wave.
+#ifndef CTN_DV_CJ
+#define CTN_DV_CJ 2
+#endif
+constexpr int DV_CJ = CTN_DV_CJ, DV_CI = 16 / DV_CJ;
+static_assert(DV_CJ == 1 || DV_CJ == 2 || DV_CJ == 4, "column blocks per column wave");
 
-// Bound-finding builds only (tools/microbench/dual_bench.hip -DCTN_DV_EXP=<bits>):
+// Bound-finding builds only (tools/microbench/dual_ws_bench.hip -DCTN_DV_EXP=<bits>):
 // bit 0 consumers skip all arithmetic (wait FULL, publish DONE), bit 1 no column part,
-// bit 2 no epilogue math.
+// bit 2 no epilogue math, bit 3 no C stores, bit 4 row waves store zeros and nothing else.
 #ifndef CTN_DV_EXP
 #define CTN_DV_EXP 0
 #endif
@@ -237,7 +246,10 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
       for (int t = t0; t < t1; ++t) {
         dv_wait<4>(fl_full[slot], gen);
         char* base = smem + slot * SLOT;
-        if constexpr (!(CTN_DV_EXP & 1)) {
+        if constexpr (CTN_DV_EXP & 16) {   // C stores only (zeros)
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb) stg16(Cg + ((size_t)t * TM + 16 * rb + lr) * p.ldc + n0 + cl, v4u{0u, 0u, 0u, 0u});
+        } else if constexpr (!(CTN_DV_EXP & 1)) {
           f32x4_t acc[2][2];
 #pragma unroll
           for (int rb = 0; rb < 2; ++rb)
@@ -280,7 +292,8 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
             const v4u cv = {pk_bf16(acc[rb][0][0], acc[rb][0][1]), pk_bf16(acc[rb][0][2], acc[rb][0][3]),
                             pk_bf16(acc[rb][1][0], acc[rb][1][1]), pk_bf16(acc[rb][1][2], acc[rb][1][3])};
             // whole 16-byte lanes straight to memory (a wave covers 16 rows x 64 B)
-            stg16(Cg + ((size_t)t * TM + 16 * rb + lr) * p.ldc + n0 + cl, (CTN_DV_DBG & 16) ? rw : cv);
+            if constexpr (!(CTN_DV_EXP & 8))
+              stg16(Cg + ((size_t)t * TM + 16 * rb + lr) * p.ldc + n0 + cl, (CTN_DV_DBG & 16) ? rw : cv);
           }
           if constexpr (NK == NORM_GLN) {
             const int m = t / tpu;
@@ -318,14 +331,15 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
   }
   if (wid < DV_NR + DV_NC) {
     // ======================= column waves =======================
-    // wave c = (wp, wn) owns dW2 blocks p in [64 wp, +64), n in [n0 + 64 wn, +64):
+    // wave c = (wp, wn) owns dW2 blocks p in [16 CI wp, +16 CI), n in [n0 + 16 CJ wn, +16 CJ):
     // dW2 += gy_tile^T . op(d)_tile, the reduction over the tile's 32 frame rows
-    const int c = wid - DV_NR, wp = c >> 1, wn = c & 1;
-    f32x4_t dacc[4][4];
+    constexpr int CI = DV_CI, CJ = DV_CJ;
+    const int c = wid - DV_NR, wp = c / (8 / CJ), wn = c % (8 / CJ);
+    f32x4_t dacc[CI][CJ];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < CI; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) dacc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < CJ; ++j) dacc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     // lane-constant LDS addresses (ctn_gemm_dual.hip's A addressing; B: RAWB=1 row-major
     // granules, block j at bbase ^ (j << 5); RAWB=0 blocks at stride DV_BST)
     const int q = lr >> 2, pp = lr & 3;
@@ -333,18 +347,18 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int row = 8 * lg + 4 * h + q;
-      abase[h] = (lg >> 1) * KB * 1024 + 2 * wp * 1024 + (pp >> 1) * 256 + (((row & 15) ^ ((pp >> 1) * 12)) << 4) +
+      abase[h] = (lg >> 1) * KB * 1024 + (CI / 2) * wp * 1024 + (pp >> 1) * 256 + (((row & 15) ^ ((pp >> 1) * 12)) << 4) +
                  (pp & 1) * 8;
-      bbase[h] = DV_RB ? dv_rbgr(row, 8 * wn + (pp >> 1)) + 8 * (pp & 1) : wn * 4 * DV_BST + dv_boff(row, 4 * pp);
+      bbase[h] = DV_RB ? dv_rbgr(row, 2 * CJ * wn + (pp >> 1)) + 8 * (pp & 1) : wn * CJ * DV_BST + dv_boff(row, 4 * pp);
     }
-    // RAWB=1: the B fragment of block j holds raw d of column 16 (4 wn + j) + lr (slice-local)
+    // RAWB=1: the B fragment of block j holds raw d of column 16 (CJ wn + j) + lr (slice-local)
     // at frame rows 8 lg .. 8 lg + 7; op(d) is applied here with the memory-side transform's
     // exact float operations (so C, Dpart and the statistics match RAWB=0 bit for bit)
-    float cg[4], cb[4];
+    float cg[CJ], cb[CJ];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      cg[j] = sgb[0][16 * (4 * wn + j) + lr];
-      cb[j] = sgb[1][16 * (4 * wn + j) + lr];
+    for (int j = 0; j < CJ; ++j) {
+      cg[j] = sgb[0][16 * (CJ * wn + j) + lr];
+      cb[j] = sgb[1][16 * (CJ * wn + j) + lr];
     }
     const float bal = p.bop.alpha[0];
     auto run = [&](auto le1) __attribute__((always_inline)) {
@@ -357,9 +371,9 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
         if constexpr (!(CTN_DV_EXP & 3)) {
           const char* a = base + OFF_A;
           const char* bb = base + OFF_B;
-          bf16x8_t bfr[4];
+          bf16x8_t bfr[CJ];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
+          for (int j = 0; j < CJ; ++j) {
             const s16x4_t lo = dv_tr(bb + (DV_RB ? bbase[0] ^ (j << 5) : bbase[0] + j * DV_BST));
             const s16x4_t hi = dv_tr(bb + (DV_RB ? bbase[1] ^ (j << 5) : bbase[1] + j * DV_BST));
             bfr[j] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -379,7 +393,7 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
             }
             const int tk = (t * TM) % Kp;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
+            for (int j = 0; j < CJ; ++j) {
               v4u v = __builtin_bit_cast(v4u, bfr[j]);
 #pragma unroll
               for (int k = 0; k < 4; ++k) {
@@ -398,12 +412,12 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
             }
           }
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
+          for (int i = 0; i < CI; ++i) {
             const int o = (i >> 1) * 1024 + (i & 1) * 512;
             const s16x4_t lo = dv_tr(a + abase[0] + o), hi = dv_tr(a + abase[1] + o);
             const bf16x8_t af = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
-            for (int j = 0; j < 4; ++j) dacc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], dacc[i][j], 0, 0, 0);
+            for (int j = 0; j < CJ; ++j) dacc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], dacc[i][j], 0, 0, 0);
           }
         }
         dv_signal(&fl_done[slot][DV_NR + c], gen);
@@ -415,15 +429,15 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
     };
     if (bal <= 1.f) run(std::true_type{});
     else run(std::false_type{});
-    // dW2 partial of this workgroup: lane holds D[(wp*4+i)*16 + 4lg + e][n0 + (wn*4+j)*16 + lr]
+    // dW2 partial of this workgroup: lane holds D[(wp*CI+i)*16 + 4lg + e][n0 + (wn*CJ+j)*16 + lr]
     float* Dp = p.Dpart + (size_t)rr * KR * p.Nout;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < CI; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = n0 + (wn * 4 + j) * 16 + lr;
+      for (int j = 0; j < CJ; ++j) {
+        const int n = n0 + (wn * CJ + j) * 16 + lr;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) Dp[(size_t)((wp * 4 + i) * 16 + 4 * lg + e) * p.Nout + n] = dacc[i][j][e];
+        for (int e = 0; e < 4; ++e) Dp[(size_t)((wp * CI + i) * 16 + 4 * lg + e) * p.Nout + n] = dacc[i][j][e];
       }
     return;
   }

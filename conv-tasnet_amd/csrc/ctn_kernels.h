@@ -319,6 +319,9 @@ struct StreamArgs {
   const float* na2 = nullptr;
   const float* nb2 = nullptr;
   const float* W2 = nullptr;
+  // ABI v7 graph replay: the call's first frame index read from device memory (written
+  // by launch_stream_set_pos before each replay) instead of `pos`
+  const long* pos_dev = nullptr;
 };
 // which: 0 encode, 1 block in (1x1, PReLU, norm 1 -> ring), 2 block out (depthwise, PReLU,
 // norm 2, 1x1, residual), 3 decode (mask, sources, frames, overlap-add)
@@ -327,5 +330,6 @@ hipError_t launch_stream(int which, const StreamArgs& a, hipStream_t s);
 // 2 block out (taps, depthwise, norms, W2 chunks, residual, ring), 3 decode mask
 // (-> sources in `frames`), 4 decoder basis + overlap-add
 hipError_t launch_stream_call_stage(int which, const StreamArgs& a, hipStream_t s);
+hipError_t launch_stream_set_pos(long* pos_dev, long pos, hipStream_t s);
 
 }  // namespace ctn

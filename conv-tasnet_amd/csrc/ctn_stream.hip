@@ -384,17 +384,18 @@ __global__ __launch_bounds__(ST_NT) void sc_block_out_kernel(StreamArgs a) {
   float* d = taps + P * H;             // [H]
   float* red = d + H;                  // [ST_NT * SC_FPB]
   const unsigned mask = (unsigned)a.R - 1u;
-  const long g = a.pos + f;
+  const long pos = a.pos_dev ? *a.pos_dev : a.pos;
+  const long g = pos + f;
   const float al1 = a.alpha1[0], al2 = a.alpha2[0];
   for (int p = 0; p < P; ++p) {
     const long src = g - (long)(P - 1 - p) * dil;           // causal taps (conv_tasnet.py:176, Chomp1d)
     float* row = taps + p * H;
-    if (src < a.pos) {                                       // an earlier call's frame (ring) or before the start
+    if (src < pos) {                                         // an earlier call's frame (ring) or before the start
       for (int j = threadIdx.x; j < H; j += ST_NT)
         row[j] = src >= 0 ? a.ring[((size_t)m * a.R + ((unsigned)src & mask)) * H + j] : 0.f;
       __syncthreads();
     } else {                                                 // this call's frame: PReLU 1 + norm 1 of its h1 row
-      const float* h = a.frames + ((size_t)m * a.K + (src - a.pos)) * H;
+      const float* h = a.frames + ((size_t)m * a.K + (src - pos)) * H;
       for (int j = threadIdx.x; j < H; j += ST_NT) {
         const float v = h[j];
         row[j] = v > 0.f ? v : al1 * v;
@@ -492,6 +493,15 @@ size_t stream_call_smem(int which, const StreamArgs& a) {
     case 3: return (size_t)(SC_FPB * a.B + a.C * SC_FPB * SC_W + SC_FPB * ST_NT) * 4;
     default: return (size_t)a.K * a.L * 4;
   }
+}
+
+__global__ void sc_set_pos_kernel(long* p, long v) {
+  if (threadIdx.x == 0) *p = v;
+}
+
+hipError_t launch_stream_set_pos(long* pos_dev, long pos, hipStream_t s) {
+  hipLaunchKernelGGL(sc_set_pos_kernel, dim3(1), dim3(64), 0, s, pos_dev, pos);
+  return hipGetLastError();
 }
 
 hipError_t launch_stream_call_stage(int which, const StreamArgs& a, hipStream_t s) {

@@ -111,6 +111,8 @@ class StreamingSeparator:
         self._mkey = None
         self.tail = None             # [M, C, stride] pending overlap-add samples
         self.frames = 0              # frames emitted so far (= pos of the next frame)
+        self._tails = None           # one_call: the tail ping-pong pair
+        self._stage = {}             # one_call: (M, K, device) -> input / output / workspace buffers
 
     @property
     def latency_samples(self) -> int:
@@ -156,16 +158,28 @@ class StreamingSeparator:
         d = self._desc(M, K)
         st = L.stream_handle(dev)
         if self.one_call:
+            # persistent staging buffers per (M, K) and a tail pair per M: the library
+            # replays one captured graph per argument set (ctn_stream_call), so equal
+            # pointers from call to call make every call after the first a replay
             nb = lib.ctn_stream_workspace_bytes(ctypes.byref(d))
-            ws = L.workspace(nb, dev)
-            out = torch.empty(M, m.C, K * self.stride, device=dev)
-            tail = torch.empty_like(self.tail)
+            sk = (M, K, dev)
+            stg = self._stage.get(sk)
+            if stg is None:
+                ns = (K - 1) * self.stride + m.L
+                stg = self._stage[sk] = dict(inp=torch.empty(M, ns, device=dev),
+                                             out=torch.empty(M, m.C, K * self.stride, device=dev),
+                                             ws=torch.empty(nb, dtype=torch.uint8, device=dev))
+            if self._tails is None or self._tails[0].shape != self.tail.shape:
+                self._tails = [self.tail, torch.empty_like(self.tail)]
+            inp = stg["inp"]
+            inp.copy_(buf[:, :inp.shape[1]])
+            tail = self._tails[1] if self.tail.data_ptr() == self._tails[0].data_ptr() else self._tails[0]
             L.check(lib.ctn_stream_call(ctypes.byref(d), ctypes.byref(self._model_struct()), self.frames,
-                                        buf.data_ptr(), buf.stride(0), self.tail.data_ptr(), tail.data_ptr(),
-                                        out.data_ptr(), ws.data_ptr(), nb, st), "ctn_stream_call")
+                                        inp.data_ptr(), inp.stride(0), self.tail.data_ptr(), tail.data_ptr(),
+                                        stg["out"].data_ptr(), stg["ws"].data_ptr(), nb, st), "ctn_stream_call")
             self.tail = tail
             self.frames += K
-            return out
+            return stg["out"].clone()
         w = torch.empty(M, K, m.N, device=dev)
         x = torch.empty(M, K, self.B, device=dev)
         L.check(lib.ctn_stream_encode(ctypes.byref(d), buf.data_ptr(), buf.stride(0), self.U.data_ptr(),

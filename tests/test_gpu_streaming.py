@@ -152,3 +152,24 @@ def test_stream_one_call_matches_stage_entries(norm, mask, C):
         outs.append(torch.cat(parts, dim=2))
     assert outs[0].shape == outs[1].shape
     assert rel(outs[0], outs[1]) < 1e-5, rel(outs[0], outs[1])
+
+
+def test_stream_graph_replay_matches_direct_launches(monkeypatch):
+    """ctn_stream_call replays a captured graph per argument set, reading the call's first
+    frame index from the workspace (CTN_STREAM_GRAPH=1, the default); with direct
+    launches (=0) every output bit is the same, over calls that reuse graphs (equal
+    chunks, both tail buffers), a ragged last chunk (another K: another graph) and a
+    second stream after flush()."""
+    import streaming
+    m = _model()
+    mix = torch.randn(3, 4000, device=DEV)
+    outs = []
+    for g in ("1", "0"):
+        monkeypatch.setenv("CTN_STREAM_GRAPH", g)
+        s = streaming.StreamingSeparator(m, max_frames=8)
+        parts = []
+        for rep in range(2):
+            parts += [s.push(mix[:, i:i + 320]) for i in range(0, 4000, 320)]
+            parts.append(s.flush())
+        outs.append(torch.cat(parts, dim=2))
+    assert torch.equal(outs[0], outs[1])

@@ -17,3 +17,8 @@ timeout -k 10 900 python -u -m pytest tests/test_gpu_tblock.py tests/test_gpu_de
 tail -2 $O/tests.log
 timeout -k 10 300 python tools/bench_streaming.py > $O/streaming.log 2>&1 || { tail $O/streaming.log; exit 1; }
 tail -25 $O/streaming.log
+export TMPDIR=/tmp
+timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench.log 2>&1 || { tail $O/bench.log; exit 1; }
+tail -1 $O/bench.log | cut -c1-250
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$O/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 2 > $O/prof.log 2>&1 || exit 1
+python tools/prof_summary.py $(ls $O/prof/*kernel_stats.csv | head -1) 7 14 | tee $O/kernel_summary.txt
