@@ -3,7 +3,10 @@ bench workload's shape (32 utterances x 4 s @ 8 kHz, paper config N=256 L=20 B=2
 H=512 P=3 X=8 R=4 gLN) through the HIP path with weights trained until the model
 separates (tests/golden/make_golden_paper_trained.py; reference SI-SNRi per utterance
 from jwr1995/Conv-TasNet's own cal_SISNRi).  bf16 activations: every utterance's
-SI-SNRi within 0.1 dB of the reference's; fp32 mode within 0.01 dB."""
+SI-SNRi within 0.1 dB of the reference's; fp32 mode within 0.01 dB.
+
+The c4 fixture (model_c4_trained.npz) does the same for the causal cLN variant (L=16)
+at c4's per-GPU dispatch: 64 utterances of 4 s @ 16 kHz (K=7999 frames, M=64)."""
 import numpy as np
 import pytest
 import torch
@@ -11,16 +14,16 @@ import torch
 import paper_fixture as PF
 from oracle import ctn_oracle as O
 
-pytestmark = [pytest.mark.gpu,
-              pytest.mark.skipif(not PF.available(), reason="model_paper_trained.npz not generated")]
+pytestmark = [pytest.mark.gpu]
+need_c2 = pytest.mark.skipif(not PF.available(), reason="model_paper_trained.npz not generated")
+need_c4 = pytest.mark.skipif(not PF.available(PF.PATH_C4), reason="model_c4_trained.npz not generated")
 
 
-def _sisnri(dtype):
+def _sisnri(dtype, path=PF.PATH, c=PF.CFG):
     import conv_tasnet as ct
     import pit_criterion as pc
-    params, mix, src, g = PF.load()
-    c = PF.CFG
-    model = ct.ConvTasNet(c.N, c.L, c.B, c.H, c.P, c.X, c.R, c.C).cuda()
+    params, mix, src, g = PF.load(path, c)
+    model = ct.ConvTasNet(c.N, c.L, c.B, c.H, c.P, c.X, c.R, c.C, norm_type=c.norm_type, causal=c.causal).cuda()
     model.load_state_dict(params)
     model.act_dtype = dtype
     lens = torch.full((mix.shape[0],), mix.shape[1], dtype=torch.int64, device="cuda")
@@ -32,6 +35,7 @@ def _sisnri(dtype):
     return got, g, float(loss)
 
 
+@need_c2
 def test_paper_trained_bf16_sisnri_within_0p1db():
     got, g, loss = _sisnri(torch.bfloat16)
     ref = g["sisnri"]
@@ -41,8 +45,27 @@ def test_paper_trained_bf16_sisnri_within_0p1db():
     assert abs(loss - float(g["loss"])) < 0.1
 
 
+@need_c2
 def test_paper_trained_fp32_sisnri_within_0p01db():
     got, g, loss = _sisnri(torch.float32)
+    d = np.abs(got - g["sisnri"])
+    assert d.max() < 0.01, d.max()
+    assert abs(loss - float(g["loss"])) < 1e-3
+
+
+@need_c4
+def test_c4_trained_bf16_sisnri_within_0p1db():
+    got, g, loss = _sisnri(torch.bfloat16, PF.PATH_C4, PF.CFG_C4)
+    ref = g["sisnri"]
+    assert ref.mean() > 3.0, "fixture model should separate"
+    d = np.abs(got - ref)
+    assert d.max() < 0.1, (d.max(), int(d.argmax()), got[d.argmax()], ref[d.argmax()])
+    assert abs(loss - float(g["loss"])) < 0.1
+
+
+@need_c4
+def test_c4_trained_fp32_sisnri_within_0p01db():
+    got, g, loss = _sisnri(torch.float32, PF.PATH_C4, PF.CFG_C4)
     d = np.abs(got - g["sisnri"])
     assert d.max() < 0.01, d.max()
     assert abs(loss - float(g["loss"])) < 1e-3

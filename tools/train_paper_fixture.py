@@ -2,12 +2,14 @@
 """Train paper-config Conv-TasNet weights on one MI355X through the HIP training step,
 for the separating paper-config parity fixture (tests/golden/make_golden_paper_trained.py).
 
-Paper config (N=256 L=20 B=256 H=512 P=3 X=8 R=4 gLN, 2 speakers), bf16 activations,
+Paper config (N=256 L=20 B=256 H=512 P=3 X=8 R=4 gLN, 2 speakers; --config c4: the
+causal cLN variant with L=16 on 1 s @ 16 kHz mixtures, BASELINE.json configs[3]), bf16 activations,
 the solver's update (clip_grad_norm_(5) + Adam lr 1e-3, src/solver.py:178-186), fresh
 synthetic speech-like mixtures of 1 s @ 8 kHz every step (synthetic.speech_like, seed =
 step).  Writes the fp32 state_dict (torch.save) and a progress log under --out.
 
     python tools/train_paper_fixture.py --steps 4000 --out gpurun_out/train
+    python tools/train_paper_fixture.py --config c4 --steps 3000 --out gpurun_out/train_c4
 """
 import argparse
 import os
@@ -27,16 +29,22 @@ import synthetic  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--config", choices=("c2", "c4"), default="c2")
     ap.add_argument("--steps", type=int, default=4000)
     ap.add_argument("--batch", type=int, default=32)
-    ap.add_argument("--samples", type=int, default=8000)
+    ap.add_argument("--samples", type=int, default=None, help="default: 1 s at the config's rate")
     ap.add_argument("--lr", type=float, default=1e-3)
     ap.add_argument("--out", default="gpurun_out/train")
     args = ap.parse_args()
     os.makedirs(args.out, exist_ok=True)
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    model = ct.ConvTasNet(256, 20, 256, 512, 3, 8, 4, 2).to(dev)
+    if args.config == "c4":
+        model = ct.ConvTasNet(256, 16, 256, 512, 3, 8, 4, 2, norm_type="cLN", causal=True).to(dev)
+        args.samples = args.samples or 16000
+    else:
+        model = ct.ConvTasNet(256, 20, 256, 512, 3, 8, 4, 2).to(dev)
+        args.samples = args.samples or 8000
     model.act_dtype = torch.bfloat16
     opt = ctn_optim.Adam(model.parameters(), lr=args.lr)
     lens = torch.full((args.batch,), args.samples, dtype=torch.int64, device=dev)
@@ -59,7 +67,7 @@ def main():
             log.write(line + "\n")
             log.flush()
     sd = {k: v.detach().float().cpu() for k, v in model.state_dict().items()}
-    torch.save(sd, os.path.join(args.out, "paper_weights.pt"))
+    torch.save(sd, os.path.join(args.out, "paper_weights.pt" if args.config == "c2" else "c4_weights.pt"))
     print(f"saved {len(sd)} tensors, final loss {run:.4f}", flush=True)
 
 
