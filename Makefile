@@ -76,3 +76,17 @@ build/dual_ws_var_%: tools/microbench/dual_ws_bench.hip $(PKG)/csrc/ctn_dual_ws.
 
 .PHONY: dualwsvar
 .PHONY: dualwsdbg
+
+# library variants for A/B runs (tools/gpu_variants.sh, loaded through CTN_HIP_LIB):
+#   make varlib VAR=<tag> VDEV="<device flags>" VDEF="<-D...>" -> build/var/lib<tag>.so
+VAR  ?= x
+VDEV ?= $(DEVFLAGS)
+VDEF ?=
+VOBJ := $(patsubst $(PKG)/csrc/%.hip,build/var/$(VAR)/%.o,$(SRC))
+build/var/$(VAR)/%.o: $(PKG)/csrc/%.hip $(HDR) Makefile
+	@mkdir -p build/var/$(VAR)
+	$(HIPCC) -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function -Iinclude $(VDEV) $(VDEF) -c $< -o $@
+build/var/lib$(VAR).so: $(VOBJ)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(VOBJ)
+varlib: build/var/lib$(VAR).so
+.PHONY: varlib

@@ -289,6 +289,9 @@ def main():
     # parameter-gradient tails on a second stream (ctn_ops._split_ok): off, the overlap
     # slowed the step by 6 % at this batch; CTN_WGRAD_STREAM=1 for A/B
     model.wgrad_stream = os.environ.get("CTN_WGRAD_STREAM", "0") == "1"
+    # parameter-gradient reductions of all blocks batched at the end of backward (on by
+    # default; CTN_DEFER_REDUCE=0 for A/B against the per-block reductions)
+    model.defer_grad_reduce = os.environ.get("CTN_DEFER_REDUCE", "1") == "1"
     if use_ddp:
         # gradients as views into the RCCL buckets (no per-step copy into the buckets),
         # one fixed graph (the reducer skips its unused-parameter search each step)
@@ -312,8 +315,10 @@ def main():
         opt.step()
         return loss
 
+    import ctn_ops
     for _ in range(args.warmup):
         step()
+    n_def0 = ctn_ops.DEFERRED_BLOCKS
     torch.cuda.synchronize(dev)
     lib = L.load()
     L.check(lib.ctn_timer_enable(args.timer_kind, args.steps * 64), "ctn_timer_enable")
@@ -340,6 +345,7 @@ def main():
         rank_ms = [round(float(x) / args.steps * 1e3, 3) for x in ts]
         elapsed = max(float(x) for x in ts)
     final_loss = float(loss)
+    deferred = (ctn_ops.DEFERRED_BLOCKS - n_def0) / args.steps
 
     if rank == 0:
         s = 4 if args.fp32 else 2
@@ -385,7 +391,10 @@ def main():
                        "per_gpu_batch": M, "global_batch": M * world, "samples": T, "frames": K,
                        "parallelism": f"dp{world}" + (" (DDP/RCCL)" if use_ddp else ""),
                        "rccl_world_size": dist.get_world_size() if use_ddp else None,
-                       "rank_ms_per_step": rank_ms},
+                       "rank_ms_per_step": rank_ms,
+                       # TemporalBlock backwards per step whose parameter-gradient reductions
+                       # ran batched at the end of backward (ctn_tblock_reduce_grads)
+                       "deferred_grad_reduce_blocks": deferred},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": {1: "gemm_ws fwd 1x1 B->H (PReLU-stats epilogue)",

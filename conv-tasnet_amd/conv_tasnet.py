@@ -89,6 +89,11 @@ class ConvTasNet(nn.Module):
         # otherwise the one-stream path runs).  Off by default: at the paper batch the
         # overlapped kernels slow each other down more than the overlap saves (§11).
         self.wgrad_stream = False
+        # True: in a plain .backward() with no gradients yet (the same conditions), each
+        # TemporalBlock leaves its parameter-gradient reductions for one batched call at
+        # the end of the backward pass (ctn_tblock_reduce_grads: a few launches instead of
+        # two per block); bit-identical gradients.
+        self.defer_grad_reduce = True
 
     def forward(self, mixture):
         """mixture [M, T] -> est_source [M, C, T] (conv_tasnet.py:45-60)."""
@@ -110,8 +115,9 @@ class ConvTasNet(nn.Module):
                 self._packs = ops.PackCache()
             packs = self._packs.get([(b.net[0].weight, b._params()[8]) for b in blocks], mixture.device)
         split = self.wgrad_stream and torch.is_grad_enabled()
+        defer = self.defer_grad_reduce and torch.is_grad_enabled() and norm != L.NORM_BN
         for blk, pk in zip(blocks, packs):
-            x = blk._forward_rows(x, fr, norm, pk, split)
+            x = blk._forward_rows(x, fr, norm, pk, split, defer)
         return ops.DecoderFn.apply(x, w_rows, fr, (T, self.N, self.L, self.B, self.C, _mask_code(self.mask_nonlinear)),
                                    sep.network[3].weight, self.decoder.basis_signals.weight)
 
@@ -275,10 +281,11 @@ class TemporalBlock(nn.Module):
         return (self.net[0].weight, self.net[1].weight, g1, b1, ds[0].weight,
                 ds[1 + off].weight, g2, b2, ds[3 + off].weight)
 
-    def _forward_rows(self, x_rows, fr, norm, pack=None, wgrad_split=False):
+    def _forward_rows(self, x_rows, fr, norm, pack=None, wgrad_split=False, defer=False):
         B, H, P, dil, causal, _ = self._geo
         bn = ops.bn_state(*self._norms()) if norm == L.NORM_BN else None
-        return ops.TBlockFn.apply(x_rows, fr, (B, H, P, dil, causal, norm, wgrad_split), pack, bn, *self._params())
+        return ops.TBlockFn.apply(x_rows, fr, (B, H, P, dil, causal, norm, wgrad_split, defer), pack, bn,
+                                  *self._params())
 
     def forward(self, x):
         """x [M, B, K] -> [M, B, K]."""

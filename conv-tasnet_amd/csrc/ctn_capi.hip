@@ -158,6 +158,7 @@ struct TbLayout {
   float2 *sums1, *sums2;
   int parts1, parts2, partsA, partsD, chunks1, chunks2;
   size_t bytes;
+  size_t part_bytes;   // split_parts: the parameter-gradient partials' own buffer
 };
 
 int tb_pad(const ctn_tblock_desc* d) {
@@ -232,9 +233,14 @@ bool tb_fused_n1(const ctn_tblock_desc* d) {
 }
 DType tb_dt(const ctn_tblock_desc* d) { return d->dtype == CTN_DTYPE_BF16 ? BF16 : F32; }
 
-TbLayout tb_layout(const ctn_tblock_desc* d, int backward, void* ws) {
+// backward, split_parts: the parameter-gradient partials (colD, alphaSlab, cpart1/2) and
+// their reduction scratch (srtmp) come from `part` (part_bytes), everything else from ws
+// (bytes) — the deferred backward (ctn_tblock_backward_deferred) keeps only `part` alive
+// until ctn_tblock_reduce_grads.
+TbLayout tb_layout(const ctn_tblock_desc* d, int backward, void* ws, void* part = nullptr, bool split_parts = false) {
   TbLayout L{};
-  Carver c(ws);
+  Carver c(ws), cpt(part);
+  Carver& cp = split_parts ? cpt : c;
   const Rows rg{d->M, d->K, d->Kp};
   const long rows = rg.rows();
   const size_t es = esize(d->dtype);
@@ -266,25 +272,26 @@ TbLayout tb_layout(const ctn_tblock_desc* d, int backward, void* ws) {
     L.slabA = c.take<double2>((size_t)G * L.partsA * sizeof(double2));
     L.partsD = dw_parts_per_group(da);
     L.slabD = c.take<double2>((size_t)G * L.partsD * sizeof(double2));
-    L.colD = c.take<float>((size_t)dw_blocks(da) * dw_col_stride(da) * sizeof(float));
+    L.colD = cp.take<float>((size_t)dw_blocks(da) * dw_col_stride(da) * sizeof(float));
     const int na = tb_fused_n1(d) ? gemm_ws_grid(tb_gemmB(d, true)) : ew_blocks(da);
-    L.alphaSlab = c.take<float>((size_t)(na > ew_blocks(da) ? na : ew_blocks(da)) * sizeof(float));
+    L.alphaSlab = cp.take<float>((size_t)(na > ew_blocks(da) ? na : ew_blocks(da)) * sizeof(float));
     L.sums1 = c.take<float2>((size_t)G * sizeof(float2));
     L.sums2 = c.take<float2>((size_t)G * sizeof(float2));
     GemmCols gc{};
     gc.g = rg; gc.P = d->B; gc.Q = d->H;
     L.chunks2 = dualA ? gemm_dual_ranges(duA) : gemm_cols_default_chunks(gc);
-    L.cpart2 = c.take<float>((size_t)L.chunks2 * d->B * d->H * sizeof(float));
+    L.cpart2 = cp.take<float>((size_t)L.chunks2 * d->B * d->H * sizeof(float));
     gc.P = d->H; gc.Q = d->B;
     L.chunks1 = dualB ? gemm_dual_ranges(duB) : gemm_cols_default_chunks(gc);
-    L.cpart1 = c.take<float>((size_t)L.chunks1 * d->B * d->H * sizeof(float));
+    L.cpart1 = cp.take<float>((size_t)L.chunks1 * d->B * d->H * sizeof(float));
     const long HB = (long)d->H * d->B, dwb = dw_blocks(da);
     const size_t ntmp = sr_tmp(L.chunks2, HB) + sr_tmp(L.chunks1, HB) + 4 * sr_tmp(dwb, d->H) +
                         sr_tmp(dwb, (long)d->H * d->P) + sr_tmp(dwb, 1) +
                         sr_tmp(ew_blocks(da), 1);
-    L.srtmp = c.take<float>(ntmp * sizeof(float));
+    L.srtmp = cp.take<float>(ntmp * sizeof(float));
   }
   L.bytes = c.off + 256;
+  L.part_bytes = split_parts ? cpt.off + 256 : 0;
   return L;
 }
 
@@ -647,7 +654,8 @@ static hipError_t fork_stream(hipStream_t from, hipStream_t to) {
 
 static int tb_backward(const ctn_tblock_desc* d, const ctn_tblock_params* p, const void* x,
                        const ctn_tblock_saved* sv, const void* gy, void* gx, const ctn_tblock_grads* gr,
-                       void* ws, size_t ws_bytes, hipStream_t s, hipStream_t sw);
+                       void* ws, size_t ws_bytes, hipStream_t s, hipStream_t sw, void* part = nullptr,
+                       size_t part_bytes = 0, bool defer = false);
 
 extern "C" int ctn_tblock_backward(const ctn_tblock_desc* d, const ctn_tblock_params* p, const void* x,
                                    const ctn_tblock_saved* sv, const void* gy, void* gx, const ctn_tblock_grads* gr,
@@ -663,16 +671,46 @@ extern "C" int ctn_tblock_backward_split(const ctn_tblock_desc* d, const ctn_tbl
                      wgrad_stream ? (hipStream_t)wgrad_stream : (hipStream_t)stream);
 }
 
-// sw: the stream of the parameter-gradient tail (== s: one stream)
+// The fixed-order reductions of every parameter gradient of a block backward (step (g)):
+// descriptors over the partials that layout L points at, into the gradients gr.
+static int tb_grad_slabs(const ctn_tblock_desc* d, const TbLayout& L, const ctn_tblock_grads* gr, SlabDesc* out) {
+  DwArgs da{};
+  da.g = Rows{d->M, d->K, d->Kp}; da.H = d->H; da.P = d->P; da.dil = d->dilation; da.pad = tb_pad(d);
+  da.norm = d->norm_type;
+  da.seg = dw_seg(da, true);
+  const int nalpha = tb_fused_n1(d) ? gemm_ws_grid(tb_gemmB(d, true)) : ew_blocks(da);
+  const int dwb = dw_blocks(da), dws = dw_col_stride(da);
+  const int HB = d->H * d->B, H = d->H;
+  out[0] = SlabDesc{L.cpart2, gr->w2, L.chunks2, HB, HB};
+  out[1] = SlabDesc{L.cpart1, gr->w1, L.chunks1, HB, HB};
+  out[2] = SlabDesc{L.colD + (2 + d->P) * H, gr->gamma2, dwb, H, dws};
+  out[3] = SlabDesc{L.colD + (3 + d->P) * H, gr->beta2, dwb, H, dws};
+  out[4] = SlabDesc{L.colD, gr->gamma1, dwb, H, dws};
+  out[5] = SlabDesc{L.colD + H, gr->beta1, dwb, H, dws};
+  out[6] = SlabDesc{L.colD + 2 * H, gr->wd, dwb, H * d->P, dws};
+  out[7] = SlabDesc{L.colD + (4 + d->P) * H, gr->alpha2, dwb, 1, dws};
+  out[8] = SlabDesc{L.alphaSlab, gr->alpha1, nalpha, 1, 1};
+  return 9;
+}
+
+// sw: the stream of the parameter-gradient tail (== s: one stream).
+// defer: the parameter-gradient partials go to `part` and step (g) is left to
+// ctn_tblock_reduce_grads.
 static int tb_backward(const ctn_tblock_desc* d, const ctn_tblock_params* p, const void* x,
                        const ctn_tblock_saved* sv, const void* gy, void* gx, const ctn_tblock_grads* gr,
-                       void* ws, size_t ws_bytes, hipStream_t s, hipStream_t sw) {
+                       void* ws, size_t ws_bytes, hipStream_t s, hipStream_t sw, void* part, size_t part_bytes,
+                       bool defer) {
   int rc = tb_check(d);
   if (rc) return rc;
   if (!p || !x || !sv || !gy || !gx || !gr) return fail(CTN_ERR_ARG, "null pointer");
-  if (d->norm_type == CTN_NORM_BN) return tb_backward_bn(d, p, x, sv, gy, gx, gr, ws, ws_bytes, s);
-  const TbLayout L = tb_layout(d, 1, ws);
+  if (d->norm_type == CTN_NORM_BN) {
+    if (defer) return fail(CTN_ERR_UNSUPPORTED, "deferred gradient reductions: gLN / cLN blocks only");
+    return tb_backward_bn(d, p, x, sv, gy, gx, gr, ws, ws_bytes, s);
+  }
+  const TbLayout L = tb_layout(d, 1, ws, part, defer);
   if (!ws || ws_bytes < L.bytes) return fail(CTN_ERR_WORKSPACE, "workspace %zu < %zu", ws_bytes, L.bytes);
+  if (defer && (!part || part_bytes < L.part_bytes))
+    return fail(CTN_ERR_WORKSPACE, "partials buffer %zu < %zu", part_bytes, L.part_bytes);
   const DType dt = d->dtype == CTN_DTYPE_BF16 ? BF16 : F32;
   const Rows rg{d->M, d->K, d->Kp};
   const int G = tb_groups(d);
@@ -803,20 +841,56 @@ static int tb_backward(const ctn_tblock_desc* d, const ctn_tblock_params* p, con
     if (sw != s) CTN_HIP(fork_stream(s, sw));
   }
   // (g) all parameter-gradient partial sums
-  const int dwb = dw_blocks(da), dws = dw_col_stride(da);
-  const int HB = d->H * d->B, H = d->H;
+  (void)nalpha;   // tb_grad_slabs recomputes the alpha-1 part count from the descriptor
+  if (defer) return CTN_OK;
   SlabBatch sb{};
-  sb.d[0] = SlabDesc{L.cpart2, gr->w2, L.chunks2, HB, HB};
-  sb.d[1] = SlabDesc{L.cpart1, gr->w1, L.chunks1, HB, HB};
-  sb.d[2] = SlabDesc{L.colD + (2 + d->P) * H, gr->gamma2, dwb, H, dws};
-  sb.d[3] = SlabDesc{L.colD + (3 + d->P) * H, gr->beta2, dwb, H, dws};
-  sb.d[4] = SlabDesc{L.colD, gr->gamma1, dwb, H, dws};
-  sb.d[5] = SlabDesc{L.colD + H, gr->beta1, dwb, H, dws};
-  sb.d[6] = SlabDesc{L.colD + 2 * H, gr->wd, dwb, H * d->P, dws};
-  sb.d[7] = SlabDesc{L.colD + (4 + d->P) * H, gr->alpha2, dwb, 1, dws};
-  sb.d[8] = SlabDesc{L.alphaSlab, gr->alpha1, nalpha, 1, 1};
-  sb.nd = 9;
+  sb.nd = tb_grad_slabs(d, L, gr, sb.d);
   CTN_HIP(launch_slab_reduce(sb, L.srtmp, sw));
+  return CTN_OK;
+}
+
+extern "C" size_t ctn_tblock_partials_bytes(const ctn_tblock_desc* d) {
+  if (tb_check(d) != CTN_OK || d->norm_type == CTN_NORM_BN) return 0;
+  return tb_layout(d, 1, nullptr, nullptr, true).part_bytes;
+}
+
+extern "C" size_t ctn_tblock_deferred_workspace_bytes(const ctn_tblock_desc* d) {
+  if (tb_check(d) != CTN_OK || d->norm_type == CTN_NORM_BN) return 0;
+  return tb_layout(d, 1, nullptr, nullptr, true).bytes;
+}
+
+extern "C" int ctn_tblock_backward_deferred(const ctn_tblock_desc* d, const ctn_tblock_params* p, const void* x,
+                                            const ctn_tblock_saved* sv, const void* gy, void* gx,
+                                            const ctn_tblock_grads* gr, void* ws, size_t ws_bytes, void* part,
+                                            size_t part_bytes, void* stream) {
+  return tb_backward(d, p, x, sv, gy, gx, gr, ws, ws_bytes, (hipStream_t)stream, (hipStream_t)stream, part,
+                     part_bytes, true);
+}
+
+extern "C" int ctn_tblock_reduce_grads(const ctn_tblock_desc* descs, const ctn_tblock_grads* grads,
+                                       void* const* parts, int n, void* stream) {
+  if (n < 0 || (n > 0 && (!descs || !grads || !parts))) return fail(CTN_ERR_ARG, "null pointer");
+  std::vector<SlabDesc> sd;
+  std::vector<float*> tmp;
+  sd.reserve((size_t)n * 9);
+  tmp.reserve((size_t)n * 9);
+  for (int i = 0; i < n; ++i) {
+    const ctn_tblock_desc* d = descs + i;
+    int rc = tb_check(d);
+    if (rc) return rc;
+    if (d->norm_type == CTN_NORM_BN) return fail(CTN_ERR_UNSUPPORTED, "deferred gradient reductions: gLN / cLN only");
+    if (!parts[i]) return fail(CTN_ERR_ARG, "null partials buffer (block %d)", i);
+    const TbLayout L = tb_layout(d, 1, nullptr, parts[i], true);
+    SlabDesc b[12];
+    const int nb = tb_grad_slabs(d, L, grads + i, b);
+    float* t[12];
+    slab_reduce_assign_tmp(b, nb, L.srtmp, t);
+    for (int k = 0; k < nb; ++k) {
+      sd.push_back(b[k]);
+      tmp.push_back(t[k]);
+    }
+  }
+  CTN_HIP(launch_slab_reduce_list(sd.data(), tmp.data(), (int)sd.size(), (hipStream_t)stream));
   return CTN_OK;
 }
 

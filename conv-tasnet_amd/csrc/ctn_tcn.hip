@@ -13,6 +13,8 @@
 // Thread layout (all three): a workgroup owns 128 frame rows of one utterance
 // (Kp % 128 == 0) and all H channels; a thread owns 8 consecutive channels
 // (one 16-byte bf16 vector) of every (256 / (H/8))-th row.
+#include <vector>
+
 #include "ctn_common.h"
 #include "ctn_kernels.h"
 
@@ -836,18 +838,22 @@ struct SrJob {
 // The grid is flat: job jb owns workgroups [wg0[jb], wg0[jb+1]), one per (slice, output
 // tile) pair, so no workgroup is launched only to exit (a (tiles, slices, jobs) grid sized
 // by the largest job launched ~70k workgroups per block backward for ~1.3k with work).
+// Up to SR_MAXJ jobs per launch (kernel arguments: ~3 KiB): a whole backward's deferred
+// reductions (ctn_tblock_reduce_grads) take a few launches instead of two per block.
+constexpr int SR_MAXJ = 64;
 struct SrBatch {
-  SrJob j[16];
-  int wg0[17];   // prefix sums of the jobs' workgroup counts
-  int ntx[16];   // output tiles per slice
+  SrJob j[SR_MAXJ];
+  int wg0[SR_MAXJ + 1];   // prefix sums of the jobs' workgroup counts
+  int ntx[SR_MAXJ];       // output tiles per slice
   int nj;
 };
 
 __global__ __launch_bounds__(256) void slab_reduce_kernel(SrBatch b) {
   __shared__ double part[4][64];
   __shared__ double part4[4][4][64];
-  int jb = 0;
-  while (jb + 1 < b.nj && (int)blockIdx.x >= b.wg0[jb + 1]) ++jb;
+  int jb = 0;   // the job owning this workgroup: binary search of the prefix sums
+  for (int step = SR_MAXJ / 2; step > 0; step >>= 1)
+    if (jb + step < b.nj && (int)blockIdx.x >= b.wg0[jb + step]) jb += step;
   const SrJob d = b.j[jb];
   const int ntx = b.ntx[jb];
   const int loc = (int)blockIdx.x - b.wg0[jb];
@@ -948,29 +954,55 @@ size_t slab_reduce_tmp_floats(const SlabBatch& b) {
   return t;
 }
 
-hipError_t launch_slab_reduce(const SlabBatch& b, float* tmp, hipStream_t s) {
-  if (b.nd <= 0) return hipSuccess;
-  SrBatch p1{}, p2{};
+// Scratch of each descriptor with more than one slice, carved from `tmp` in descriptor
+// order (slab_reduce_tmp_floats' sizing); null where one pass suffices or tmp is null.
+void slab_reduce_assign_tmp(const SlabDesc* d, int n, float* tmp, float** out) {
   size_t off = 0;
-  auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-  for (int i = 0; i < b.nd; ++i) {
-    const SlabDesc& d = b.d[i];
-    const int ns = (d.nparts + SR_SLICE - 1) / SR_SLICE;
-    const bool v4 = d.n % 4 == 0 && d.pstride % 4 == 0 && a16(d.src) && a16(d.dst);
-    if (ns <= 1 || !tmp) {
-      // single pass straight into dst (also the fallback when no scratch is given)
-      p2.j[p2.nj++] = SrJob{d.src, d.dst, d.nparts, d.n, d.pstride, 1, v4 ? 1 : 0};
-    } else {
-      float* t = tmp + off;
-      off += (size_t)ns * d.n;
-      const bool v4t = v4 && a16(t);
-      p1.j[p1.nj++] = SrJob{d.src, t, d.nparts, d.n, d.pstride, ns, v4t ? 1 : 0};
-      p2.j[p2.nj++] = SrJob{t, d.dst, ns, d.n, d.n, 1, v4t ? 1 : 0};
+  for (int i = 0; i < n; ++i) {
+    const int ns = (d[i].nparts + SR_SLICE - 1) / SR_SLICE;
+    out[i] = nullptr;
+    if (ns > 1 && tmp) {
+      out[i] = tmp + off;
+      off += (size_t)ns * d[i].n;
     }
   }
-  hipError_t e = sr_launch(p1, s);
-  if (e != hipSuccess) return e;
-  return sr_launch(p2, s);
+}
+
+// Every first pass (slice partials) of the list, then every second pass, SR_MAXJ jobs per
+// launch.  Each descriptor's per-output summation order is that of launch_slab_reduce.
+hipError_t launch_slab_reduce_list(const SlabDesc* descs, float* const* tmps, int n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  std::vector<SrJob> j1, j2;
+  auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  for (int i = 0; i < n; ++i) {
+    const SlabDesc& d = descs[i];
+    const int ns = (d.nparts + SR_SLICE - 1) / SR_SLICE;
+    const bool v4 = d.n % 4 == 0 && d.pstride % 4 == 0 && a16(d.src) && a16(d.dst);
+    float* t = tmps ? tmps[i] : nullptr;
+    if (ns <= 1 || !t) {
+      // single pass straight into dst (also the fallback when no scratch is given)
+      j2.push_back(SrJob{d.src, d.dst, d.nparts, d.n, d.pstride, 1, v4 ? 1 : 0});
+    } else {
+      const bool v4t = v4 && a16(t);
+      j1.push_back(SrJob{d.src, t, d.nparts, d.n, d.pstride, ns, v4t ? 1 : 0});
+      j2.push_back(SrJob{t, d.dst, ns, d.n, d.n, 1, v4t ? 1 : 0});
+    }
+  }
+  for (const std::vector<SrJob>* js : {&j1, &j2}) {
+    for (size_t k = 0; k < js->size(); k += SR_MAXJ) {
+      SrBatch b{};
+      for (size_t i = k; i < js->size() && b.nj < SR_MAXJ; ++i) b.j[b.nj++] = (*js)[i];
+      const hipError_t e = sr_launch(b, s);
+      if (e != hipSuccess) return e;
+    }
+  }
+  return hipSuccess;
+}
+
+hipError_t launch_slab_reduce(const SlabBatch& b, float* tmp, hipStream_t s) {
+  float* tmps[12];
+  slab_reduce_assign_tmp(b.d, b.nd, tmp, tmps);
+  return launch_slab_reduce_list(b.d, tmps, b.nd, s);
 }
 
 // fp32 [O][I] weight -> storage-type copy Ws [O][I] and/or transpose Wt [I][O], one

@@ -14,7 +14,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CTN_HIP_LIB", os.path.join(_HERE, "libctn_hip.so"))
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 DTYPE_F32, DTYPE_BF16 = 0, 1
 NORM_GLN, NORM_CLN, NORM_BN = 0, 1, 2
@@ -122,6 +122,12 @@ _SIGS = {
                                            c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "ctn_tblock_backward_split": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                                  c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p]),
+    "ctn_tblock_partials_bytes": (c_size_t, [c_void_p]),
+    "ctn_tblock_deferred_workspace_bytes": (c_size_t, [c_void_p]),
+    "ctn_tblock_backward_deferred": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                                    c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_size_t,
+                                                    c_void_p]),
+    "ctn_tblock_reduce_grads": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, ctypes.c_int, c_void_p]),
     "ctn_encoder_workspace_bytes": (c_size_t, [c_void_p, ctypes.c_int]),
     "ctn_encoder_forward": (ctypes.c_int, [c_void_p] + [c_void_p] * 8 + [c_void_p, c_size_t, c_void_p]),
     "ctn_encoder_backward": (ctypes.c_int, [c_void_p] + [c_void_p] * 13 + [c_void_p, c_size_t, c_void_p]),

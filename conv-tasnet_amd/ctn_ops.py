@@ -5,6 +5,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 from dataclasses import dataclass
 
 import torch
@@ -159,17 +160,63 @@ def _join_wgrad(device, key):
     torch.cuda.current_stream(device).wait_stream(_wgrad_stream(device))
 
 
-def _split_ok(ctx) -> bool:
-    """The parameter-gradient tail may run on the side stream and write .grad directly
-    only when nothing can observe the gradients before the backward pass ends: a plain
+# parameter -> the live forward records (TBlockFn contexts) that use it.  A late .grad
+# write is safe only for a parameter that exactly one pending TemporalBlock backward uses:
+# with two (the model run twice before one backward, a shared weight) the other use's
+# AccumulateGrad would add into a gradient that the late write then overwrites.
+_USES = weakref.WeakKeyDictionary()
+
+
+class _Use:
+    """Token held by one TBlockFn context; dies with its autograd graph."""
+    __slots__ = ("__weakref__",)
+
+
+def _register_uses(ctx, params):
+    ctx.use_token = tok = _Use()
+    for p in params:
+        s = _USES.get(p)
+        if s is None:
+            s = _USES[p] = weakref.WeakSet()
+        s.add(tok)
+
+
+DEFERRED_BLOCKS = 0   # block backwards that took the deferred path (tests, bench)
+# (device, autograd graph task) -> the deferred block backwards of that backward pass,
+# reduced together by _flush_deferred at its end (ctn_tblock_reduce_grads)
+_DEFER_PENDING = {}
+
+
+def _flush_deferred(key):
+    """End of the backward pass: every deferred block's parameter gradients in one batched
+    reduction, on the stream the block backwards ran on, before any consumer of .grad."""
+    entries = _DEFER_PENDING.pop(key, None)
+    dev, task = key
+    for k in [k for k in _DEFER_PENDING if k[0] == dev and k[1] < task]:
+        del _DEFER_PENDING[k]          # left by a backward pass that raised before its end
+    if not entries:
+        return
+    lib = L.load()
+    n = len(entries)
+    descs = (L.TBlockDesc * n)(*[e[0] for e in entries])
+    grads = (L.TBlockGrads * n)(*[e[1] for e in entries])
+    parts = (ctypes.c_void_p * n)(*[e[2].data_ptr() for e in entries])
+    L.check(lib.ctn_tblock_reduce_grads(descs, grads, parts, n, entries[0][4]), "ctn_tblock_reduce_grads")
+
+
+def _grads_unobserved(ctx) -> bool:
+    """.grad of this block's parameters may be written late (after this node) only when
+    nothing can observe the gradients before the backward pass ends: a plain
     .backward() that will accumulate into every one of these leaves (not
     autograd.grad), no gradient yet (no accumulation), no hooks, fp32 contiguous
     leaves, no torch.distributed (DDP hooks read gradients as they arrive)."""
-    if not ctx.wgrad_split or torch.is_grad_enabled():
+    if torch.is_grad_enabled() or not hasattr(ctx, "param_refs"):
         return False
     if torch.distributed.is_available() and torch.distributed.is_initialized():
         return False
     for p, node in zip(ctx.param_refs, ctx.acc_nodes):
+        if len(_USES.get(p, ())) != 1:    # another pending use of this parameter
+            return False
         if (node is None or p.grad is not None or p.dtype != torch.float32 or not p.is_contiguous()
                 or p._backward_hooks or getattr(p, "_post_accumulate_grad_hooks", None)):
             return False
@@ -181,6 +228,12 @@ def _split_ok(ctx) -> bool:
     return True
 
 
+def _split_ok(ctx) -> bool:
+    """The parameter-gradient tail may run on the side stream and write .grad directly
+    only when the gradients are unobservable until the backward pass ends."""
+    return ctx.wgrad_split and _grads_unobserved(ctx)
+
+
 class TBlockFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, fr: Frames, cfg: tuple, pack, bn, w1, a1, g1, b1, wd, a2, g2, b2, w2):
@@ -188,13 +241,18 @@ class TBlockFn(torch.autograd.Function):
         WeightPacks, or None.
         bn: BatchNorm state for norm_type BN (bn_state()), else None.
         cfg[6] (optional, ConvTasNet.wgrad_stream): let the backward run its
-        parameter-gradient tail on a second stream when that is unobservable (_split_ok)."""
+        parameter-gradient tail on a second stream when that is unobservable (_split_ok).
+        cfg[7] (optional, ConvTasNet.defer_grad_reduce): leave the parameter-gradient
+        reductions to one batched call at the end of the backward pass when that is
+        unobservable (_grads_unobserved; not with the side stream)."""
         B, H, P, dil, causal, norm = cfg[:6]
         ctx.wgrad_split = len(cfg) > 6 and bool(cfg[6])
-        if ctx.wgrad_split:
+        ctx.defer = len(cfg) > 7 and bool(cfg[7]) and norm != L.NORM_BN
+        if ctx.wgrad_split or ctx.defer:
             ctx.param_refs = (w1, a1, g1, b1, wd, a2, g2, b2, w2)
             ctx.acc_nodes = tuple(torch.autograd.graph.get_gradient_edge(t).node if t.requires_grad and t.is_leaf
                                   else None for t in ctx.param_refs)
+            _register_uses(ctx, ctx.param_refs)
         lib = L.load()
         L.require_device(x, "TemporalBlock")
         x = x.contiguous()
@@ -234,6 +292,8 @@ class TBlockFn(torch.autograd.Function):
         gx = torch.empty_like(x)
         grads = [torch.empty_like(p) for p in params]
         gstruct = L.TBlockGrads(*[g.data_ptr() for g in grads])
+        if ctx.defer and not ctx.wgrad_split and _grads_unobserved(ctx):
+            return TBlockFn._backward_deferred(ctx, lib, desc, pstruct, saved, x, gy, gx, grads, gstruct)
         nb = lib.ctn_tblock_workspace_bytes(ctypes.byref(desc), 1)
         ws = L.workspace(nb, x.device)
         if not _split_ok(ctx):
@@ -260,6 +320,34 @@ class TBlockFn(torch.autograd.Function):
             _WGRAD_PENDING.add(key)
             dev = x.device
             torch.autograd.Variable._execution_engine.queue_callback(lambda: _join_wgrad(dev, key))
+        return (gx, None, None, None, None) + (None,) * 9
+
+    @staticmethod
+    def _backward_deferred(ctx, lib, desc, pstruct, saved, x, gy, gx, grads, gstruct):
+        """gx now; the parameter gradients' partials go to their own buffer and one batched
+        reduction at the end of the backward pass writes .grad (_flush_deferred)."""
+        global DEFERRED_BLOCKS
+        DEFERRED_BLOCKS += 1
+        dev = x.device
+        stream = L.stream_handle(dev)
+        nb = lib.ctn_tblock_deferred_workspace_bytes(ctypes.byref(desc))
+        ws = L.workspace(nb, dev)
+        npart = lib.ctn_tblock_partials_bytes(ctypes.byref(desc))
+        part = L.workspace(npart, dev)
+        L.check(lib.ctn_tblock_backward_deferred(ctypes.byref(desc), ctypes.byref(pstruct), x.data_ptr(),
+                                                 ctypes.byref(saved), gy.data_ptr(), gx.data_ptr(),
+                                                 ctypes.byref(gstruct), ws.data_ptr(), nb, part.data_ptr(), npart,
+                                                 stream),
+                "ctn_tblock_backward_deferred")
+        for p, g in zip(ctx.param_refs, grads):
+            p.grad = g
+        key = (dev, torch._C._current_graph_task_id())
+        lst = _DEFER_PENDING.get(key)
+        if lst is None:
+            lst = _DEFER_PENDING[key] = []
+            torch.autograd.Variable._execution_engine.queue_callback(lambda: _flush_deferred(key))
+        # the partials, gradients and their descriptors stay alive until the flush
+        lst.append((L.TBlockDesc(*ctx.desc), gstruct, part, grads, stream))
         return (gx, None, None, None, None) + (None,) * 9
 
 

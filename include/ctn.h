@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define CTN_ABI_VERSION 7
+#define CTN_ABI_VERSION 8
 
 typedef enum { CTN_DTYPE_F32 = 0, CTN_DTYPE_BF16 = 1 } ctn_dtype;
 /* CTN_NORM_BN: torch.nn.BatchNorm1d, chose_norm's fallback branch (conv_tasnet.py:302-303) */
@@ -149,6 +149,25 @@ int ctn_tblock_backward_split(const ctn_tblock_desc* d, const ctn_tblock_params*
                               const ctn_tblock_saved* saved, const void* gy, void* gx,
                               const ctn_tblock_grads* g, void* ws, size_t ws_bytes, void* stream,
                               void* wgrad_stream);
+
+/* ABI v8: the same backward with every parameter-gradient reduction left for later, so
+ * that one call can reduce all blocks of a backward pass (a few launches instead of two
+ * per block).  The fixed-order partial sums go to `part` (ctn_tblock_partials_bytes(d)
+ * bytes; ws then needs only ctn_tblock_deferred_workspace_bytes(d)); the gradients in
+ * `g` are NOT written by this call.  gLN / cLN blocks only (BN: CTN_ERR_UNSUPPORTED).
+ * Replaces, for a whole backward pass, the per-block gradient writes of the reference's
+ * TemporalBlock backward (src/conv_tasnet.py:217-263, autograd).                       */
+size_t ctn_tblock_partials_bytes(const ctn_tblock_desc* d);
+size_t ctn_tblock_deferred_workspace_bytes(const ctn_tblock_desc* d);
+int ctn_tblock_backward_deferred(const ctn_tblock_desc* d, const ctn_tblock_params* p, const void* x,
+                                 const ctn_tblock_saved* saved, const void* gy, void* gx,
+                                 const ctn_tblock_grads* g, void* ws, size_t ws_bytes, void* part,
+                                 size_t part_bytes, void* stream);
+/* Write the gradients g[i] of n deferred block backwards from their partials parts[i]
+ * (each part[i] unmodified since its ctn_tblock_backward_deferred call; descs[i] the same
+ * descriptor).  Bit-identical to the per-block reductions of ctn_tblock_backward.       */
+int ctn_tblock_reduce_grads(const ctn_tblock_desc* descs, const ctn_tblock_grads* g, void* const* parts, int n,
+                            void* stream);
 
 /* -------------------------------------------------------------------------
  * Front of the network: Encoder (src/conv_tasnet.py:97-117: ReLU(Conv1d(1,N,L,

@@ -1,0 +1,160 @@
+"""Deferred parameter-gradient reductions (ConvTasNet.defer_grad_reduce,
+ctn_tblock_backward_deferred + ctn_tblock_reduce_grads): each TemporalBlock backward
+leaves its fixed-order partial sums in a buffer and one batched call at the end of the
+backward pass reduces all blocks, with the per-output summation order of the per-block
+reductions — so every gradient is bit-identical to the immediate path.  Cases where a
+late .grad would be observable (autograd.grad, accumulation, hooks) take the immediate
+path.  GPU only."""
+import os
+import sys
+
+import pytest
+import torch
+
+from conftest import ROOT
+
+sys.path.insert(0, os.path.join(ROOT, "conv-tasnet_amd"))
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _model(norm="gLN", causal=False, dims=(64, 16, 64, 128, 3, 3, 2, 2), dtype=torch.bfloat16):
+    import conv_tasnet as ct
+    torch.manual_seed(0)
+    m = ct.ConvTasNet(*dims, norm_type=norm, causal=causal).to(DEV)
+    m.act_dtype = dtype
+    return m
+
+
+def _grads(m, mix, src, defer):
+    import pit_criterion as pc
+    m.defer_grad_reduce = defer
+    m.zero_grad(set_to_none=True)
+    est = m(mix)
+    loss = pc.cal_loss(src, est, torch.full((mix.shape[0],), mix.shape[1], device=DEV))[0]
+    loss.backward()
+    return [p.grad.detach().clone() for p in m.parameters()]
+
+
+@pytest.mark.parametrize("norm,causal,dtype", [("gLN", False, torch.bfloat16), ("cLN", True, torch.bfloat16),
+                                               ("gLN", False, torch.float32)])
+def test_deferred_backward_bit_identical(norm, causal, dtype):
+    import ctn_ops
+    m = _model(norm, causal, dtype=dtype)
+    torch.manual_seed(1)
+    mix = torch.randn(3, 4000, device=DEV)
+    src = torch.randn(3, 2, 4000, device=DEV)
+    ref = _grads(m, mix, src, False)
+    n0 = ctn_ops.DEFERRED_BLOCKS
+    for _ in range(3):   # repeated: the partial buffers are reused safely
+        got = _grads(m, mix, src, True)
+        assert ctn_ops.DEFERRED_BLOCKS - n0 == 6 * (_ + 1)   # every block of every pass
+        for a, b in zip(ref, got):
+            assert torch.equal(a, b)
+    assert not ctn_ops._DEFER_PENDING
+
+
+def test_deferred_backward_bit_identical_bench_shape():
+    """The bench's c2 dispatch: paper config, 32 utterances of 4 s @ 8 kHz, bf16."""
+    m = _model(dims=(256, 20, 256, 512, 3, 8, 4, 2))
+    torch.manual_seed(3)
+    mix = torch.randn(32, 32000, device=DEV)
+    src = torch.randn(32, 2, 32000, device=DEV)
+    ref = _grads(m, mix, src, False)
+    got = _grads(m, mix, src, True)
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b)
+
+
+def test_deferred_not_used_when_observable():
+    """autograd.grad w.r.t. the parameters, accumulation into existing gradients and
+    gradient hooks all see the same values as the immediate path."""
+    import pit_criterion as pc
+    m = _model()
+    torch.manual_seed(2)
+    mix = torch.randn(2, 4000, device=DEV)
+    src = torch.randn(2, 2, 4000, device=DEV)
+    lens = torch.full((2,), 4000, device=DEV)
+    params = list(m.parameters())
+    ref = _grads(m, mix, src, False)
+
+    m.defer_grad_reduce = True
+    m.zero_grad(set_to_none=True)
+    gs = torch.autograd.grad(pc.cal_loss(src, m(mix), lens)[0], params)
+    assert all(p.grad is None for p in params)
+    for a, b in zip(ref, gs):
+        assert torch.equal(a, b)
+
+    m.zero_grad(set_to_none=True)
+    pc.cal_loss(src, m(mix), lens)[0].backward()
+    pc.cal_loss(src, m(mix), lens)[0].backward()
+    for a, p in zip(ref, params):
+        assert torch.allclose(p.grad, 2 * a, rtol=1e-6, atol=1e-7)
+
+    m.zero_grad(set_to_none=True)
+    w = next(m.separator.blocks()).net[0].weight
+    seen = []
+    h = w.register_hook(lambda g: seen.append(g.detach().clone()))
+    pc.cal_loss(src, m(mix), lens)[0].backward()
+    h.remove()
+    i = [q is w for q in params].index(True)
+    assert torch.equal(seen[0], ref[i]) and torch.equal(w.grad, ref[i])
+
+
+def test_deferred_after_failed_backward():
+    """A backward pass that raises after some blocks deferred leaves no stale state that
+    changes the next backward's gradients."""
+    import ctn_ops
+    import pit_criterion as pc
+    m = _model()
+    torch.manual_seed(4)
+    mix = torch.randn(2, 4000, device=DEV)
+    src = torch.randn(2, 2, 4000, device=DEV)
+    lens = torch.full((2,), 4000, device=DEV)
+    ref = _grads(m, mix, src, False)
+
+    class Boom(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x):
+            return x.clone()
+
+        @staticmethod
+        def backward(ctx, g):
+            raise RuntimeError("boom")
+
+    m.defer_grad_reduce = True
+    m.zero_grad(set_to_none=True)
+    n0 = ctn_ops.DEFERRED_BLOCKS
+    # the failing node is the mixture's own: it runs after every block's backward
+    est = m(Boom.apply(mix.clone().requires_grad_(True)))
+    loss = pc.cal_loss(src, est, lens)[0]
+    with pytest.raises(RuntimeError, match="boom"):
+        loss.backward()
+    assert ctn_ops.DEFERRED_BLOCKS > n0        # the blocks did defer before the failure
+    assert ctn_ops._DEFER_PENDING               # ... and their reduction never ran
+    del est, loss
+    got = _grads(m, mix, src, True)
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b)
+    assert len(ctn_ops._DEFER_PENDING) == 0
+
+
+def test_deferred_not_used_for_a_twice_used_model():
+    """Two forwards before one backward: every block parameter has two pending uses, so
+    the immediate path accumulates both."""
+    import ctn_ops
+    import pit_criterion as pc
+    m = _model()
+    torch.manual_seed(5)
+    mix = torch.randn(2, 4000, device=DEV)
+    src = torch.randn(2, 2, 4000, device=DEV)
+    lens = torch.full((2,), 4000, device=DEV)
+    ref = _grads(m, mix, src, False)
+    m.defer_grad_reduce = True
+    m.zero_grad(set_to_none=True)
+    n0 = ctn_ops.DEFERRED_BLOCKS
+    (pc.cal_loss(src, m(mix), lens)[0] + pc.cal_loss(src, m(mix), lens)[0]).backward()
+    assert ctn_ops.DEFERRED_BLOCKS == n0
+    for a, p in zip(ref, m.parameters()):
+        assert torch.allclose(p.grad, 2 * a, rtol=1e-6, atol=1e-7)
