@@ -164,7 +164,9 @@ def _join_wgrad(device, key):
 # write is safe only for a parameter that exactly one pending TemporalBlock backward uses:
 # with two (the model run twice before one backward, a shared weight) the other use's
 # AccumulateGrad would add into a gradient that the late write then overwrites.
-_USES = weakref.WeakKeyDictionary()
+# Keyed by id(parameter) with a weak reference to it (a WeakKeyDictionary would compare
+# tensors with ==); an entry whose parameter died is replaced on the next registration.
+_USES = {}
 
 
 class _Use:
@@ -175,10 +177,15 @@ class _Use:
 def _register_uses(ctx, params):
     ctx.use_token = tok = _Use()
     for p in params:
-        s = _USES.get(p)
-        if s is None:
-            s = _USES[p] = weakref.WeakSet()
-        s.add(tok)
+        e = _USES.get(id(p))
+        if e is None or e[0]() is not p:
+            e = _USES[id(p)] = (weakref.ref(p), weakref.WeakSet())
+        e[1].add(tok)
+
+
+def _pending_uses(p) -> int:
+    e = _USES.get(id(p))
+    return len(e[1]) if e is not None and e[0]() is p else 0
 
 
 DEFERRED_BLOCKS = 0   # block backwards that took the deferred path (tests, bench)
@@ -215,7 +222,7 @@ def _grads_unobserved(ctx) -> bool:
     if torch.distributed.is_available() and torch.distributed.is_initialized():
         return False
     for p, node in zip(ctx.param_refs, ctx.acc_nodes):
-        if len(_USES.get(p, ())) != 1:    # another pending use of this parameter
+        if _pending_uses(p) != 1:    # another pending use of this parameter
             return False
         if (node is None or p.grad is not None or p.dtype != torch.float32 or not p.is_contiguous()
                 or p._backward_hooks or getattr(p, "_post_accumulate_grad_hooks", None)):
