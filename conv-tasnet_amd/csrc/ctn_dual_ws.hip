@@ -47,14 +47,15 @@ constexpr int DV_NT = (DV_ND + DV_NMW) * 64;     // 1024 threads
 constexpr int DV_KB = 8, DV_KR = 256;            // reduction of the row part (gy channels)
 constexpr int DV_NS = 128;                       // output channels per slice
 constexpr int DV_GRID = 256;
-// Slot layout.  CTN_DV_RAWB=1 (default): the B image holds the raw d slice exactly as the
-// LDS-DMA lands it (row-major, 16-byte granules swizzled per row); the column waves apply
-// PReLU + norm + affine to their B fragments, the row waves read raw d from it, and no
-// other image exists, so a slot is 24.8 KB and the ring holds 6 tiles.  CTN_DV_RAWB=0:
-// the memory waves write op(d) into a separate B image from a raw-d image R (33 KB slots,
-// ring of 4).
+// Slot layout.  CTN_DV_RAWB=0 (default): the memory waves write op(d) into a B image from
+// a raw-d image R (33 KB slots, ring of 4), so op(d) is computed once per element.
+// CTN_DV_RAWB=1: the B image holds the raw d slice exactly as the LDS-DMA lands it
+// (row-major, 16-byte granules swizzled per row); the column waves apply PReLU + norm +
+// affine to their B fragments (each fragment by 8 / CJ of them), the row waves read raw d
+// from it, a slot is 24.8 KB and the ring holds 6 tiles.  The SIMDs' VALU issue is what
+// the kernel spends its time on: RAWB=0 measured 93.9 against 100.7 us.
 #ifndef CTN_DV_RAWB
-#define CTN_DV_RAWB 1
+#define CTN_DV_RAWB 0
 #endif
 constexpr bool DV_RB = CTN_DV_RAWB;
 #ifndef CTN_DV_NSL
@@ -127,6 +128,22 @@ CTN_DEV void dv_vmwait(int n) {
     default: asm volatile("s_waitcnt vmcnt(35)" ::: "memory"); break;
   }
 #undef CTN_VMW
+}
+
+// counted wait with a compile-time count (the steady state of the ring: a runtime switch
+// over the count compiles to ~300 scalar instructions per tile)
+template <int N> CTN_DEV void dv_vmwait_c() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// PReLU max / min without the NaN-quieting copy IEEE mode adds to fmaxf / fminf of a value
+// not known to be canonical (operands here are finite activations)
+template <bool LE1> CTN_DEV float dv_prelu(float x, float al) {
+  const float ax = x * al;
+  float r;
+  if constexpr (LE1) asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(ax));
+  else asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(ax));
+  return r;
 }
 
 CTN_DEV s16x4_t dv_tr(const char* p) {
@@ -265,7 +282,10 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
                 acc[rb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wf[nb][kb]),
                                                                       __builtin_bit_cast(bf16x8_t, b), acc[rb][nb], 0, 0, 0);
             }
-          // ---- epilogue: norm-2 backward sums, C image (16 bytes per lane and row)
+          // ---- epilogue: norm-2 backward sums, C image (16 bytes per lane and row).
+          // Sum ga * hat a = rstd * Sum ga * a - mean * rstd * Sum ga over the lane's 8
+          // channels of a row (one (mean, rstd) per row): the per-element work is the PReLU,
+          // ga and two accumulations; the statistics enter once per row.
           float s1[2] = {0.f, 0.f}, q1[2] = {0.f, 0.f};
 #pragma unroll
           for (int rb = 0; rb < 2; ++rb) {
@@ -279,15 +299,15 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
             float f[8];
             unpack_bf16x8(rw, f);
             if constexpr (!(CTN_DV_EXP & 4)) {
+              float qa = 0.f;
 #pragma unroll
               for (int e = 0; e < 8; ++e) {
-                const float x = f[e];
-                const float a = LE1 ? fmaxf(x, x * eal) : fminf(x, x * eal);   // PReLU
-                const float ah = ok ? fmaf(a, rs, ms) : 0.f;                     // hat a
+                const float a = dv_prelu<LE1>(f[e], eal);
                 const float ga = acc[rb][e >> 2][e & 3] * gam[e];
                 s1[rb] += ga;
-                q1[rb] = fmaf(ga, ah, q1[rb]);
+                qa = fmaf(ga, a, qa);
               }
+              q1[rb] = ok ? fmaf(qa, rs, s1[rb] * ms) : 0.f;
             }
             const v4u cv = {pk_bf16(acc[rb][0][0], acc[rb][0][1]), pk_bf16(acc[rb][0][2], acc[rb][0][3]),
                             pk_bf16(acc[rb][1][0], acc[rb][1][1]), pk_bf16(acc[rb][1][2], acc[rb][1][3])};
@@ -398,8 +418,8 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
 #pragma unroll
               for (int k = 0; k < 4; ++k) {
                 float x0 = __uint_as_float(v[k] << 16), x1 = __uint_as_float(v[k] & 0xffff0000u);
-                x0 = LE1 ? fmaxf(x0, x0 * bal) : fminf(x0, x0 * bal);   // PReLU
-                x1 = LE1 ? fmaxf(x1, x1 * bal) : fminf(x1, x1 * bal);
+                x0 = dv_prelu<LE1>(x0, bal);
+                x1 = dv_prelu<LE1>(x1, bal);
                 x0 = fmaf(x0 - mu[2 * k], rs[2 * k] * cg[j], cb[j]);
                 x1 = fmaf(x1 - mu[2 * k + 1], rs[2 * k + 1] * cg[j], cb[j]);
                 if constexpr (NK == NORM_CLN) {   // padded frames: statistics not finite
@@ -483,7 +503,7 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
   const uint32_t soff = st_lane ? (uint32_t)((NK == NORM_CLN && !DV_RB ? 8 * mw * 8 : 0) + lane * 4) : DU_OOB;
   const bool st_wave = !DV_RB || mw == 0;
   const float bal = p.bop.alpha[0];
-  const int G = st_wave ? 7 : 6;   // DMA instructions per wave and tile
+  // DMA instructions per wave and tile: 7 (st_wave), else 6 (RAWB=1 waves 1..3)
 
   auto dma = [&](int t) __attribute__((always_inline)) {
     char* base = smem + ((t - t0) % NSL) * SLOT;
@@ -495,6 +515,17 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
     for (int h = 0; h < 2; ++h) du_dma16(rD, base + (DV_RB ? OFF_B : OFF_R) + (2 * mw + h) * 1024, doff[h], t * TM * p.ldb * 2);
     if (st_wave) du_dma4(rS, base + OFF_ST + (DV_RB ? 0 : mw * 256), soff, NK == NORM_GLN ? (t / tpu) * 8 : t * TM * 8);
   };
+  // the lane's gamma2 / beta2 (its granule's 8 channels, per piece) stay in registers
+  float tgam[2][8], tbet[2][8];
+  if constexpr (!DV_RB) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        tgam[h][e] = p.bop.gamma[n0 + 8 * dgr[h] + e];
+        tbet[h][e] = p.bop.beta[n0 + 8 * dgr[h] + e];
+      }
+  }
   auto transform = [&](auto le1, int t, char* base) __attribute__((always_inline)) {
     constexpr bool LE1 = decltype(le1)::value;
     const int tk = (t * TM) % Kp;
@@ -503,18 +534,13 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
       const int row = drow[h];
       v4u v = *reinterpret_cast<const v4u*>(base + OFF_R + (2 * mw + h) * 1024 + lane * 16);
       const float2 st = *reinterpret_cast<const float2*>(base + OFF_ST + mw * 256 + (NK == NORM_GLN ? 0 : (row & 7) * 8));
-      float gam[8], bet[8];
-      *reinterpret_cast<float4*>(gam) = *reinterpret_cast<const float4*>(&sgb[0][8 * dgr[h]]);
-      *reinterpret_cast<float4*>(gam + 4) = *reinterpret_cast<const float4*>(&sgb[0][8 * dgr[h] + 4]);
-      *reinterpret_cast<float4*>(bet) = *reinterpret_cast<const float4*>(&sgb[1][8 * dgr[h]]);
-      *reinterpret_cast<float4*>(bet + 4) = *reinterpret_cast<const float4*>(&sgb[1][8 * dgr[h] + 4]);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         float x0 = __uint_as_float(v[e] << 16), x1 = __uint_as_float(v[e] & 0xffff0000u);
-        x0 = LE1 ? fmaxf(x0, x0 * bal) : fminf(x0, x0 * bal);   // PReLU
-        x1 = LE1 ? fmaxf(x1, x1 * bal) : fminf(x1, x1 * bal);
-        x0 = fmaf(x0 - st.x, st.y * gam[2 * e], bet[2 * e]);
-        x1 = fmaf(x1 - st.x, st.y * gam[2 * e + 1], bet[2 * e + 1]);
+        x0 = dv_prelu<LE1>(x0, bal);
+        x1 = dv_prelu<LE1>(x1, bal);
+        x0 = fmaf(x0 - st.x, st.y * tgam[h][2 * e], tbet[h][2 * e]);
+        x1 = fmaf(x1 - st.x, st.y * tgam[h][2 * e + 1], tbet[h][2 * e + 1]);
         v[e] = pk_bf16(x0, x1);
       }
       if constexpr (NK == NORM_CLN)   // padded frames: statistics not finite
@@ -530,12 +556,15 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
     for (int t = t0; t < t1; ++t) {
       const int later = t1 - 1 - t < PF - 1 ? t1 - 1 - t : PF - 1;   // DMA groups issued after tile t's
       char* base = smem + slot * SLOT;
-      if constexpr (DV_RB) {
-        dv_vmwait(G * later);
+      // tile t's DMA group done: every group issued after it may stay in flight (steady
+      // state: PF - 1 of them, a compile-time count; the tail waits for all)
+      if (later == PF - 1) {
+        if (!DV_RB || st_wave) dv_vmwait_c<7 * (PF - 1)>();
+        else dv_vmwait_c<6 * (PF - 1)>();
       } else {
-        vmwait23(G * later);
-        transform(le1, t, base);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
+      if constexpr (!DV_RB) transform(le1, t, base);
       dv_signal(&fl_full[slot][mw], gen);
       const int tn = t + PF;
       if (tn < t1) {
