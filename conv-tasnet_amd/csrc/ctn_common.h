@@ -141,6 +141,12 @@ CTN_DEV void du_vmwait(int n) {
   }
 }
 // the same up to vmcnt(23) (the WS GEMM's ring)
+// counted wait with a compile-time count: the steady state of a DMA ring (the runtime
+// switch below compiles to a chain of scalar compares and branches per call)
+template <int N> CTN_DEV void vmwait_c() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 CTN_DEV void vmwait23(int n) {
 #define CTN_VMW(k) \
   case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
@@ -317,11 +323,26 @@ CTN_DEV f32x2_t pmax(f32x2_t a, f32x2_t b) { return __builtin_elementwise_max(a,
 CTN_DEV f32x2_t pmin(f32x2_t a, f32x2_t b) { return __builtin_elementwise_min(a, b); }
 #endif
 CTN_DEV f32x2_t pfma(f32x2_t a, f32x2_t b, f32x2_t c) { return __builtin_elementwise_fma(a, b, c); }
-// PReLU of a pair with one shared alpha: max(x, a*x) when a <= 1, min(x, a*x) when a > 1
-// (both exact: the branch is chosen once per kernel, LE1 = (alpha <= 1))
+// PReLU with one shared alpha: max(x, a*x) when a <= 1, min(x, a*x) when a > 1 (both
+// exact: the branch is chosen once per kernel, LE1 = (alpha <= 1)).  One v_max_f32 /
+// v_min_f32 per element: fmaxf / fminf in IEEE mode first copy every operand not known to
+// be canonical through another v_max_f32 (NaN quieting), a third of the PReLU's
+// instructions; the operands here are finite activations, for which the results agree bit
+// for bit.  (CTN_IEEE_MAX=1 keeps the round-2 builtin forms for A/B.)
+template <bool LE1> CTN_DEV float prelu_nq(float x, float a) {
+  const float ax = x * a;
+  float r;
+  if constexpr (LE1) asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(ax));
+  else asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(ax));
+  return r;
+}
 template <bool LE1> CTN_DEV f32x2_t prelu2(f32x2_t x, float a) {
+#if CTN_IEEE_MAX
   const f32x2_t ax = x * a;
   return LE1 ? pmax(x, ax) : pmin(x, ax);
+#else
+  return f32x2_t{prelu_nq<LE1>(x.x, a), prelu_nq<LE1>(x.y, a)};
+#endif
 }
 
 // Block-wide sum of NV doubles; result valid in thread 0.  `red` must hold

@@ -136,15 +136,7 @@ template <int N> CTN_DEV void dv_vmwait_c() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
-// PReLU max / min without the NaN-quieting copy IEEE mode adds to fmaxf / fminf of a value
-// not known to be canonical (operands here are finite activations)
-template <bool LE1> CTN_DEV float dv_prelu(float x, float al) {
-  const float ax = x * al;
-  float r;
-  if constexpr (LE1) asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(ax));
-  else asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(ax));
-  return r;
-}
+template <bool LE1> CTN_DEV float dv_prelu(float x, float al) { return prelu_nq<LE1>(x, al); }
 
 CTN_DEV s16x4_t dv_tr(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(p));

@@ -656,7 +656,12 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
       for (int i = 0; i < WS_DR - 1; ++i) dma(t0 + i);
       if constexpr (!CTN_WS_EARLY) ready_all();
       for (int t = t0; t < t1; ++t) {
-        vmwait23(NFW * mn(WS_DR - 2, t1 - 1 - t) + SPT * mn(WS_DR - 1, t - t0));
+        {
+          constexpr int NST = NFW * (WS_DR - 2) + SPT * (WS_DR - 1);   // steady state
+          const int n = NFW * mn(WS_DR - 2, t1 - 1 - t) + SPT * mn(WS_DR - 1, t - t0);
+          if (n == NST) vmwait_c<NST>();
+          else vmwait23(n);
+        }
         lds_barrier();
         if (t > t0) cln_final(t - 1);
         dma(t + WS_DR - 1);
