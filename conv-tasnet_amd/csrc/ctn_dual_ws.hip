@@ -47,15 +47,15 @@ constexpr int DV_NT = (DV_ND + DV_NMW) * 64;     // 1024 threads
 constexpr int DV_KB = 8, DV_KR = 256;            // reduction of the row part (gy channels)
 constexpr int DV_NS = 128;                       // output channels per slice
 constexpr int DV_GRID = 256;
-// Slot layout.  CTN_DV_RAWB=0 (default): the memory waves write op(d) into a B image from
-// a raw-d image R (33 KB slots, ring of 4), so op(d) is computed once per element.
-// CTN_DV_RAWB=1: the B image holds the raw d slice exactly as the LDS-DMA lands it
-// (row-major, 16-byte granules swizzled per row); the column waves apply PReLU + norm +
-// affine to their B fragments (each fragment by 8 / CJ of them), the row waves read raw d
-// from it, a slot is 24.8 KB and the ring holds 6 tiles.  The SIMDs' VALU issue is what
-// the kernel spends its time on: RAWB=0 measured 93.9 against 100.7 us.
+// Slot layout.  CTN_DV_RAWB=1 (default): the B image holds the raw d slice exactly as the
+// LDS-DMA lands it (row-major, 16-byte granules swizzled per row); the column waves apply
+// PReLU + norm + affine to their B fragments (each fragment by the CJ waves that share
+// it), the row waves read raw d from it, a slot is 24.8 KB and the ring holds 6 tiles.
+// CTN_DV_RAWB=0: the memory waves write op(d) into a B image from a raw-d image R (33 KB
+// slots, ring of 4) — op(d) once per element, but in the producer's critical path:
+// 99.5 us against 79.5 us (RAWB=1, CJ=1) at the bench shape.
 #ifndef CTN_DV_RAWB
-#define CTN_DV_RAWB 0
+#define CTN_DV_RAWB 1
 #endif
 constexpr bool DV_RB = CTN_DV_RAWB;
 #ifndef CTN_DV_NSL
@@ -65,9 +65,9 @@ constexpr int DV_NSL = CTN_DV_NSL;               // LDS ring slots (NSL - 1 tile
 // Column-wave split of the 256 x 128 dW2 slice: each of the 8 waves owns CJ 16-column
 // blocks x (16 / CJ) 16-row blocks (64 accumulator registers either way).  Fewer column
 // blocks per wave means fewer waves share (and, RAWB=1, transform) each B fragment, at
-// the price of more A fragment reads per wave.
+// the price of more A fragment reads per wave: CJ=1 79.5 us, CJ=2 85.0 (bench shape).
 #ifndef CTN_DV_CJ
-#define CTN_DV_CJ 2
+#define CTN_DV_CJ 1
 #endif
 constexpr int DV_CJ = CTN_DV_CJ, DV_CI = 16 / DV_CJ;
 static_assert(DV_CJ == 1 || DV_CJ == 2 || DV_CJ == 4, "column blocks per column wave");
@@ -275,9 +275,8 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
                                                                       __builtin_bit_cast(bf16x8_t, b), acc[rb][nb], 0, 0, 0);
             }
           // ---- epilogue: norm-2 backward sums, C image (16 bytes per lane and row).
-          // Sum ga * hat a = rstd * Sum ga * a - mean * rstd * Sum ga over the lane's 8
-          // channels of a row (one (mean, rstd) per row): the per-element work is the PReLU,
-          // ga and two accumulations; the statistics enter once per row.
+          // (Summing ga * a and scaling by rstd once per row saves one FMA per element but
+          // cancels when |mean| >> the spread of a: not used.)
           float s1[2] = {0.f, 0.f}, q1[2] = {0.f, 0.f};
 #pragma unroll
           for (int rb = 0; rb < 2; ++rb) {
@@ -291,15 +290,14 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
             float f[8];
             unpack_bf16x8(rw, f);
             if constexpr (!(CTN_DV_EXP & 4)) {
-              float qa = 0.f;
 #pragma unroll
               for (int e = 0; e < 8; ++e) {
                 const float a = dv_prelu<LE1>(f[e], eal);
+                const float ah = ok ? fmaf(a, rs, ms) : 0.f;   // hat a
                 const float ga = acc[rb][e >> 2][e & 3] * gam[e];
                 s1[rb] += ga;
-                qa = fmaf(ga, a, qa);
+                q1[rb] = fmaf(ga, ah, q1[rb]);
               }
-              q1[rb] = ok ? fmaf(qa, rs, s1[rb] * ms) : 0.f;
             }
             const v4u cv = {pk_bf16(acc[rb][0][0], acc[rb][0][1]), pk_bf16(acc[rb][0][2], acc[rb][0][3]),
                             pk_bf16(acc[rb][1][0], acc[rb][1][1]), pk_bf16(acc[rb][1][2], acc[rb][1][3])};

@@ -399,12 +399,13 @@ def test_model_c4_shape_bf16_gradients_vs_oracle():
     e_r = O.model_forward(cfg, mix[sel], pr)
     (e_r * G[sel]).sum().backward()
     pg = dict(model.named_parameters())
-    worst = 0.0
+    errs = {}
     for n, shape in O.param_shapes(cfg):
         if shape == (1,):
             continue   # PReLU alpha in bf16: cancellation-heavy scalar (see test_gpu_tblock.py)
         g, gr = pg[n].grad.detach().cpu().reshape(pr[n].grad.shape), pr[n].grad
-        e = rel(g, gr)
-        worst = max(worst, e)
-        assert e < 0.1, (n, e)
-    print("c4 weight gradients, worst relative L2:", worst)
+        errs[n] = rel(g, gr)
+    top = sorted(errs.items(), key=lambda kv: -kv[1])[:8]
+    print("c4 weight gradients, largest relative L2:", [(n, round(float(e), 4)) for n, e in top])
+    bad = {n: e for n, e in errs.items() if e >= 0.1}
+    assert not bad, bad
