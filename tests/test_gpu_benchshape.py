@@ -377,10 +377,20 @@ def test_model_c4_shape_bf16_gradients_vs_oracle():
     """c4's per-GPU dispatch (causal cLN, L=16, 64 utterances of 4 s @ 16 kHz, K=7999,
     bf16), backward of sum(G * est) with G nonzero only on utterances {0, 32, 63}: cLN,
     the causal depthwise conv and the 1x1 convs act per frame / per utterance, so the
-    weight gradients are the fp32 oracle's on those three utterances alone.  Every
-    weight gradient (conv / linear weights, norm gamma / beta) within 0.1 relative L2 —
-    a misplaced cLN statistic of one row range in the M=64 backward would move them
-    by far more (conv_tasnet.py:176,289,307-329)."""
+    weight gradients are those of the three utterances alone.
+
+    (1) Dispatch: the M=64 bf16 gradients against the same three utterances run alone
+    through the same bf16 path (M=3): every per-row quantity is the same arithmetic, only
+    the fixed-order partial sums group differently, so they agree to 1e-3 relative L2 — a
+    misplaced cLN statistic or row range of the M=64 grids (64 x 8064 rows, 12-25 tiles
+    per workgroup, range-end clamps) would move them by far more (conv_tasnet.py:176,
+    289,307-329).
+    (2) Values: the fp32 oracle on the three utterances.  With RANDOM weights the bf16
+    activations (x, h1, d and the data gradients stored in bf16 through 32 blocks) move
+    the weight gradients of the deep blocks by 0.13-0.19 relative L2 and the front-end
+    ones (input cLN, bottleneck) by about 0.11-0.13 (measured, profiles/r04); the bound
+    here is 0.25 — the north-star check of the bf16 numerics at c4 is the separating
+    trained-weight fixture (tests/test_gpu_paper_trained.py, SI-SNRi within 0.1 dB)."""
     import synthetic
     cfg_d = dict(PAPER, L=16, norm_type="cLN", causal=True)
     cfg = O.Cfg(**cfg_d)
@@ -391,21 +401,29 @@ def test_model_c4_shape_bf16_gradients_vs_oracle():
     gen = torch.Generator().manual_seed(7)
     G = torch.zeros(M, 2, T)
     G[sel] = torch.randn(len(sel), 2, T, generator=gen)
-    model = _hip_model(cfg_d, params, torch.bfloat16)
-    est = model(mix.to(DEV))
-    model.zero_grad()
-    (est.float() * G.to(DEV)).sum().backward()
+
+    def hip_grads(mx, gg):
+        model = _hip_model(cfg_d, params, torch.bfloat16)
+        est = model(mx.to(DEV))
+        model.zero_grad()
+        (est.float() * gg.to(DEV)).sum().backward()
+        return {n: p.grad.detach().cpu().clone() for n, p in model.named_parameters()}
+
+    g64 = hip_grads(mix, G)
+    g3 = hip_grads(mix[sel], G[sel])
     pr = {n: v.clone().requires_grad_(True) for n, v in params.items()}
     e_r = O.model_forward(cfg, mix[sel], pr)
     (e_r * G[sel]).sum().backward()
-    pg = dict(model.named_parameters())
-    errs = {}
+    disp, val = {}, {}
     for n, shape in O.param_shapes(cfg):
         if shape == (1,):
             continue   # PReLU alpha in bf16: cancellation-heavy scalar (see test_gpu_tblock.py)
-        g, gr = pg[n].grad.detach().cpu().reshape(pr[n].grad.shape), pr[n].grad
-        errs[n] = rel(g, gr)
-    top = sorted(errs.items(), key=lambda kv: -kv[1])[:8]
-    print("c4 weight gradients, largest relative L2:", [(n, round(float(e), 4)) for n, e in top])
-    bad = {n: e for n, e in errs.items() if e >= 0.1}
+        disp[n] = rel(g64[n], g3[n])
+        val[n] = rel(g64[n].reshape(pr[n].grad.shape), pr[n].grad)
+    top = lambda d: [(n, round(float(e), 4)) for n, e in sorted(d.items(), key=lambda kv: -kv[1])[:6]]
+    print("c4 M=64 vs M=3 (same bf16 path), largest relative L2:", top(disp))
+    print("c4 M=64 bf16 vs fp32 oracle, largest relative L2:", top(val))
+    bad = {n: e for n, e in disp.items() if e >= 1e-3}
+    assert not bad, bad
+    bad = {n: e for n, e in val.items() if e >= 0.25}
     assert not bad, bad
