@@ -299,11 +299,15 @@ class TBlockFn(torch.autograd.Function):
         gx = torch.empty_like(x)
         grads = [torch.empty_like(p) for p in params]
         gstruct = L.TBlockGrads(*[g.data_ptr() for g in grads])
-        if ctx.defer and not ctx.wgrad_split and _grads_unobserved(ctx):
+        late_ok = (ctx.defer or ctx.wgrad_split) and _grads_unobserved(ctx)
+        # this context's use of the parameters is spent once its backward runs (a graph
+        # kept alive by a returned loss must not count as a pending use in the next step)
+        ctx.use_token = None
+        if ctx.defer and not ctx.wgrad_split and late_ok:
             return TBlockFn._backward_deferred(ctx, lib, desc, pstruct, saved, x, gy, gx, grads, gstruct)
         nb = lib.ctn_tblock_workspace_bytes(ctypes.byref(desc), 1)
         ws = L.workspace(nb, x.device)
-        if not _split_ok(ctx):
+        if not (ctx.wgrad_split and late_ok):
             L.check(lib.ctn_tblock_backward(ctypes.byref(desc), ctypes.byref(pstruct), x.data_ptr(),
                                             ctypes.byref(saved), gy.data_ptr(), gx.data_ptr(), ctypes.byref(gstruct),
                                             ws.data_ptr(), nb, L.stream_handle(x.device)),

@@ -158,3 +158,27 @@ def test_deferred_not_used_for_a_twice_used_model():
     assert ctn_ops.DEFERRED_BLOCKS == n0
     for a, p in zip(ref, m.parameters()):
         assert torch.allclose(p.grad, 2 * a, rtol=1e-6, atol=1e-7)
+
+
+def test_deferred_with_previous_graph_alive():
+    """The bench's pattern: each step returns its loss, which keeps the previous step's
+    graph alive while the next step runs; a spent backward's parameter uses must not
+    block the deferral of the next one."""
+    import ctn_ops
+    import pit_criterion as pc
+    m = _model()
+    torch.manual_seed(6)
+    mix = torch.randn(2, 4000, device=DEV)
+    src = torch.randn(2, 2, 4000, device=DEV)
+    lens = torch.full((2,), 4000, device=DEV)
+    ref = _grads(m, mix, src, False)
+    m.defer_grad_reduce = True
+    loss = None
+    for _ in range(3):
+        n0 = ctn_ops.DEFERRED_BLOCKS
+        m.zero_grad(set_to_none=True)
+        loss = pc.cal_loss(src, m(mix), lens)[0]
+        loss.backward()
+        assert ctn_ops.DEFERRED_BLOCKS - n0 == 6
+        for a, p in zip(ref, m.parameters()):
+            assert torch.equal(a, p.grad)

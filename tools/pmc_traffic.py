@@ -18,7 +18,7 @@ from collections import defaultdict
 KINDS = {   # bench.py timer kinds -> kernel name (bf16 throughput mode)
     "1": "ctn::gemm_ws_kernel<0, 0, 1, 2, 8, 16, 2, 1>",
     "2": "ctn::dw_fwd_kernel<unsigned short, 0, 3, false>",
-    "3": "ctn::gemm_dual_kernel<8, 8, 2, 3, 2, 0, 4>",
+    "3": "gemm_dual_ws_kernel<0, ",   # the wave-specialised pair-A dual (gLN)
 }
 
 
