@@ -72,6 +72,12 @@ constexpr int DV_NSL = CTN_DV_NSL;               // LDS ring slots (NSL - 1 tile
 constexpr int DV_CJ = CTN_DV_CJ, DV_CI = 16 / DV_CJ;
 static_assert(DV_CJ == 1 || DV_CJ == 2 || DV_CJ == 4, "column blocks per column wave");
 
+// Row waves: A fragments read LA k-steps ahead of their MFMAs
+#ifndef CTN_DV_LA
+#define CTN_DV_LA 1
+#endif
+constexpr int DV_LA = CTN_DV_LA;
+
 // Bound-finding builds only (tools/microbench/dual_ws_bench.hip -DCTN_DV_EXP=<bits>):
 // bit 0 consumers skip all arithmetic (wait FULL, publish DONE), bit 1 no column part,
 // bit 2 no epilogue math, bit 3 no C stores, bit 4 row waves store zeros and nothing else.
@@ -264,16 +270,38 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
           for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
             for (int nb = 0; nb < 2; ++nb) acc[rb][nb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+          // the A fragments of k-step kb + LA are read while the MFMAs of kb run (the
+          // interleave pinned below: the register-pressure scheduler would otherwise pull
+          // each read down to its MFMAs and expose every read's latency)
+          constexpr int LA = DV_LA;
+          v4u bw[LA + 1][2];
+          auto rd = [&](int kb) __attribute__((always_inline)) {
 #pragma unroll
-          for (int kb = 0; kb < KB; ++kb)
+            for (int rb = 0; rb < 2; ++rb)
+              bw[kb % (LA + 1)][rb] = *reinterpret_cast<const v4u*>(base + OFF_A + rb * KB * 1024 + rbase + kb * 1024);
+          };
+#pragma unroll
+          for (int kb = 0; kb < LA && kb < KB; ++kb) rd(kb);
+#pragma unroll
+          for (int kb = 0; kb < KB; ++kb) {
+            if (kb + LA < KB) rd(kb + LA);
 #pragma unroll
             for (int rb = 0; rb < 2; ++rb) {
-              const v4u b = *reinterpret_cast<const v4u*>(base + OFF_A + rb * KB * 1024 + rbase + kb * 1024);
+              const v4u b = bw[kb % (LA + 1)][rb];
 #pragma unroll
               for (int nb = 0; nb < 2; ++nb)
                 acc[rb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wf[nb][kb]),
                                                                       __builtin_bit_cast(bf16x8_t, b), acc[rb][nb], 0, 0, 0);
             }
+          }
+          if constexpr (LA > 0) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 2 * (LA < KB ? LA : KB), 0);
+#pragma unroll
+            for (int kb = 0; kb < KB; ++kb) {
+              if (kb + LA < KB) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+              __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+            }
+          }
           // ---- epilogue: norm-2 backward sums, C image (16 bytes per lane and row).
           // (Summing ga * a and scaling by rstd once per row saves one FMA per element but
           // cancels when |mean| >> the spread of a: not used.)

@@ -189,26 +189,51 @@ def _pending_uses(p) -> int:
 
 
 DEFERRED_BLOCKS = 0   # block backwards that took the deferred path (tests, bench)
-# (device, autograd graph task) -> the deferred block backwards of that backward pass,
-# reduced together by _flush_deferred at its end (ctn_tblock_reduce_grads)
-_DEFER_PENDING = {}
 
 
-def _flush_deferred(key):
+class _TaskState:
+    """What one backward pass (device, autograd graph task) leaves for its end: the
+    contexts whose parameter uses it spent, and its deferred block backwards."""
+    __slots__ = ("ctxs", "deferred")
+
+    def __init__(self):
+        self.ctxs, self.deferred = [], []
+
+
+_TASKS = {}
+
+
+def _task_state(dev) -> "_TaskState":
+    key = (dev, torch._C._current_graph_task_id())
+    st = _TASKS.get(key)
+    if st is None:
+        st = _TASKS[key] = _TaskState()
+        torch.autograd.Variable._execution_engine.queue_callback(lambda: _end_of_backward(key))
+    return st
+
+
+def _end_of_backward(key):
     """End of the backward pass: every deferred block's parameter gradients in one batched
-    reduction, on the stream the block backwards ran on, before any consumer of .grad."""
-    entries = _DEFER_PENDING.pop(key, None)
+    reduction, on the stream the block backwards ran on, before any consumer of .grad; then
+    the pass's parameter uses are spent (a graph kept alive by a returned loss must not
+    count as a pending use in the next step; released here and not at each node, because
+    an immediate node's gradient is accumulated only after the node returns)."""
+    st = _TASKS.pop(key, None)
     dev, task = key
-    for k in [k for k in _DEFER_PENDING if k[0] == dev and k[1] < task]:
-        del _DEFER_PENDING[k]          # left by a backward pass that raised before its end
-    if not entries:
+    for k in [k for k in _TASKS if k[0] == dev and k[1] < task]:
+        del _TASKS[k]          # left by a backward pass that raised before its end
+    if st is None:
         return
-    lib = L.load()
-    n = len(entries)
-    descs = (L.TBlockDesc * n)(*[e[0] for e in entries])
-    grads = (L.TBlockGrads * n)(*[e[1] for e in entries])
-    parts = (ctypes.c_void_p * n)(*[e[2].data_ptr() for e in entries])
-    L.check(lib.ctn_tblock_reduce_grads(descs, grads, parts, n, entries[0][4]), "ctn_tblock_reduce_grads")
+    entries = st.deferred
+    if entries:
+        lib = L.load()
+        n = len(entries)
+        descs = (L.TBlockDesc * n)(*[e[0] for e in entries])
+        grads = (L.TBlockGrads * n)(*[e[1] for e in entries])
+        parts = (ctypes.c_void_p * n)(*[e[2].data_ptr() for e in entries])
+        L.check(lib.ctn_tblock_reduce_grads(descs, grads, parts, n, entries[0][4]), "ctn_tblock_reduce_grads")
+    for ctx in st.ctxs:
+        ctx.use_token = None
 
 
 def _grads_unobserved(ctx) -> bool:
@@ -300,9 +325,8 @@ class TBlockFn(torch.autograd.Function):
         grads = [torch.empty_like(p) for p in params]
         gstruct = L.TBlockGrads(*[g.data_ptr() for g in grads])
         late_ok = (ctx.defer or ctx.wgrad_split) and _grads_unobserved(ctx)
-        # this context's use of the parameters is spent once its backward runs (a graph
-        # kept alive by a returned loss must not count as a pending use in the next step)
-        ctx.use_token = None
+        if getattr(ctx, "use_token", None) is not None:
+            _task_state(x.device).ctxs.append(ctx)   # this use is spent at the pass's end
         if ctx.defer and not ctx.wgrad_split and late_ok:
             return TBlockFn._backward_deferred(ctx, lib, desc, pstruct, saved, x, gy, gx, grads, gstruct)
         nb = lib.ctn_tblock_workspace_bytes(ctypes.byref(desc), 1)
@@ -336,7 +360,7 @@ class TBlockFn(torch.autograd.Function):
     @staticmethod
     def _backward_deferred(ctx, lib, desc, pstruct, saved, x, gy, gx, grads, gstruct):
         """gx now; the parameter gradients' partials go to their own buffer and one batched
-        reduction at the end of the backward pass writes .grad (_flush_deferred)."""
+        reduction at the end of the backward pass writes .grad (_end_of_backward)."""
         global DEFERRED_BLOCKS
         DEFERRED_BLOCKS += 1
         dev = x.device
@@ -352,13 +376,8 @@ class TBlockFn(torch.autograd.Function):
                 "ctn_tblock_backward_deferred")
         for p, g in zip(ctx.param_refs, grads):
             p.grad = g
-        key = (dev, torch._C._current_graph_task_id())
-        lst = _DEFER_PENDING.get(key)
-        if lst is None:
-            lst = _DEFER_PENDING[key] = []
-            torch.autograd.Variable._execution_engine.queue_callback(lambda: _flush_deferred(key))
-        # the partials, gradients and their descriptors stay alive until the flush
-        lst.append((L.TBlockDesc(*ctx.desc), gstruct, part, grads, stream))
+        # the partials, gradients and their descriptors stay alive until the pass's end
+        _task_state(dev).deferred.append((L.TBlockDesc(*ctx.desc), gstruct, part, grads, stream))
         return (gx, None, None, None, None) + (None,) * 9
 
 

@@ -52,7 +52,7 @@ def test_deferred_backward_bit_identical(norm, causal, dtype):
         assert ctn_ops.DEFERRED_BLOCKS - n0 == 6 * (_ + 1)   # every block of every pass
         for a, b in zip(ref, got):
             assert torch.equal(a, b)
-    assert not ctn_ops._DEFER_PENDING
+    assert not ctn_ops._TASKS
 
 
 def test_deferred_backward_bit_identical_bench_shape():
@@ -132,12 +132,12 @@ def test_deferred_after_failed_backward():
     with pytest.raises(RuntimeError, match="boom"):
         loss.backward()
     assert ctn_ops.DEFERRED_BLOCKS > n0        # the blocks did defer before the failure
-    assert ctn_ops._DEFER_PENDING               # ... and their reduction never ran
+    assert ctn_ops._TASKS                       # ... and their reduction never ran
     del est, loss
     got = _grads(m, mix, src, True)
     for a, b in zip(ref, got):
         assert torch.equal(a, b)
-    assert len(ctn_ops._DEFER_PENDING) == 0
+    assert len(ctn_ops._TASKS) == 0
 
 
 def test_deferred_not_used_for_a_twice_used_model():
