@@ -170,8 +170,12 @@ _USES = {}
 
 
 class _Use:
-    """Token held by one TBlockFn context; dies with its autograd graph."""
-    __slots__ = ("__weakref__",)
+    """Token held by one TBlockFn context; dies with its autograd graph, or is spent
+    (dead) at the end of the backward pass that ran the context's backward."""
+    __slots__ = ("__weakref__", "dead")
+
+    def __init__(self):
+        self.dead = False
 
 
 def _register_uses(ctx, params):
@@ -185,7 +189,7 @@ def _register_uses(ctx, params):
 
 def _pending_uses(p) -> int:
     e = _USES.get(id(p))
-    return len(e[1]) if e is not None and e[0]() is p else 0
+    return sum(1 for t in e[1] if not t.dead) if e is not None and e[0]() is p else 0
 
 
 DEFERRED_BLOCKS = 0   # block backwards that took the deferred path (tests, bench)
@@ -194,10 +198,10 @@ DEFERRED_BLOCKS = 0   # block backwards that took the deferred path (tests, benc
 class _TaskState:
     """What one backward pass (device, autograd graph task) leaves for its end: the
     contexts whose parameter uses it spent, and its deferred block backwards."""
-    __slots__ = ("ctxs", "deferred")
+    __slots__ = ("tokens", "deferred")
 
     def __init__(self):
-        self.ctxs, self.deferred = [], []
+        self.tokens, self.deferred = [], []   # weak references: a dropped graph's tokens die
 
 
 _TASKS = {}
@@ -232,8 +236,10 @@ def _end_of_backward(key):
         grads = (L.TBlockGrads * n)(*[e[1] for e in entries])
         parts = (ctypes.c_void_p * n)(*[e[2].data_ptr() for e in entries])
         L.check(lib.ctn_tblock_reduce_grads(descs, grads, parts, n, entries[0][4]), "ctn_tblock_reduce_grads")
-    for ctx in st.ctxs:
-        ctx.use_token = None
+    for r in st.tokens:
+        t = r()
+        if t is not None:
+            t.dead = True
 
 
 def _grads_unobserved(ctx) -> bool:
@@ -326,7 +332,7 @@ class TBlockFn(torch.autograd.Function):
         gstruct = L.TBlockGrads(*[g.data_ptr() for g in grads])
         late_ok = (ctx.defer or ctx.wgrad_split) and _grads_unobserved(ctx)
         if getattr(ctx, "use_token", None) is not None:
-            _task_state(x.device).ctxs.append(ctx)   # this use is spent at the pass's end
+            _task_state(x.device).tokens.append(weakref.ref(ctx.use_token))   # spent at the pass's end
         if ctx.defer and not ctx.wgrad_split and late_ok:
             return TBlockFn._backward_deferred(ctx, lib, desc, pstruct, saved, x, gy, gx, grads, gstruct)
         nb = lib.ctn_tblock_workspace_bytes(ctypes.byref(desc), 1)
