@@ -86,6 +86,36 @@ CTN_DEV void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// Generation words in LDS (ring hand-offs between waves of one workgroup, no barrier):
+// a wave publishes `gen` in its word of a slot after its own LDS operations on the slot
+// completed (flag_signal), and a consumer polls the N words of a slot until all reach
+// `gen` (flag_wait; wave-uniform by readfirstlane, bounded at ~0.2 s so a protocol
+// error ends the launch with wrong results instead of a wave that never finishes).
+// Volatile accesses keep their address space only through an LDS-typed pointer (a
+// generic one becomes a FLAT access, whose wait drains every outstanding global load).
+typedef __attribute__((address_space(3))) volatile v4u flag_v4u;
+typedef __attribute__((address_space(3))) volatile uint32_t flag_u32;
+template <int N> CTN_DEV void flag_wait(const uint32_t* f, uint32_t gen) {
+  static_assert(N % 4 == 0, "generation words per slot: whole 16-byte reads");
+  const flag_v4u* fl = (const flag_v4u*)(f);
+  for (uint32_t it = 0; it < (1u << 22); ++it) {
+    uint32_t mn = 0xffffffffu;
+#pragma unroll
+    for (int i = 0; i < N / 4; ++i) {
+      const v4u a = fl[i];
+      mn = min(mn, min(min(a[0], a[1]), min(a[2], a[3])));
+    }
+    if (__builtin_amdgcn_readfirstlane(mn) >= gen) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  asm volatile("" ::: "memory");
+}
+CTN_DEV void flag_signal(uint32_t* f, uint32_t gen) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  *(flag_u32*)(f) = gen;
+  asm volatile("" ::: "memory");
+}
+
 // Buffer resources and LDS-DMA (the dual GEMM and the plain column GEMM)
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 CTN_DEV rsrc_t du_rsrc(const void* p, long bytes) {

@@ -45,6 +45,14 @@ constexpr int WS_WAVES = 8, WS_TM = 16, WS_GRID = CTN_WS_GRID;
 #define CTN_WS_DR 4
 #endif
 constexpr int WS_DR = CTN_WS_DR;
+// The LDS-DMA ring's hand-offs (gLN, no in-kernel cLN finalize): 1 (default) = generation
+// words per slot and wave instead of one workgroup barrier per tile — a wave starts tile
+// t's MFMAs once every wave's DMA of tile t has landed and refills a slot once every wave
+// has read it, so the waves drift within the ring (one wave's epilogue beside another's
+// MFMAs) instead of running MFMA, VALU and stores in lockstep.
+#ifndef CTN_WS_FLAGS
+#define CTN_WS_FLAGS 1
+#endif
 constexpr int WS_FOLD_MAX = 512;   // utterances whose gLN operand stats a workgroup holds in LDS
 
 // Bound-finding experiments only (tools/microbench): bit 0 drops the output
@@ -141,6 +149,9 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
   __shared__ double2 scln[CLN_FIN ? 2 * TM * WV : 1];
   constexpr bool WDMA = CTN_WS_DMA && OPK == OP_PLAIN && !SWP && EPI != EPI_RESID && EPI != EPI_NORM_BWD;
   __shared__ __attribute__((aligned(16))) char sA[WDMA ? WS_DR : 2][TM * KR * 2];
+  constexpr bool WFL = WDMA && CTN_WS_FLAGS && !CLN_FIN && WV % 4 == 0;   // flag-ring hand-offs
+  __shared__ __attribute__((aligned(16))) uint32_t fl_full[WFL ? WS_DR : 1][WFL ? WV : 4];
+  __shared__ __attribute__((aligned(16))) uint32_t fl_done[WFL ? WS_DR : 1][WFL ? WV : 4];
   __shared__ float sgam[EPI == EPI_NORM_BWD ? NB * 16 * WV : 1];
   // gLN operand statistics, one pair per utterance, finalized here (StatFold)
   constexpr bool FOLDS = NK == NORM_GLN && OPK != OP_PLAIN;
@@ -653,8 +664,40 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
       auto mn = [](int a, int b) { return a < b ? a : b; };
       f32x4_t acc[MB][NB];
       fold_stats();
+      if constexpr (WFL) {
+        if (tid < WS_DR * WV) {
+          (&fl_full[0][0])[tid] = 0u;
+          (&fl_done[0][0])[tid] = 0u;
+        }
+        __syncthreads();
+      }
       for (int i = 0; i < WS_DR - 1; ++i) dma(t0 + i);
       if constexpr (!CTN_WS_EARLY) ready_all();
+      if constexpr (WFL) {
+        // tile t in slot t % WS_DR, generation (t - t0) / WS_DR + 1 of that slot
+        for (int t = t0; t < t1; ++t) {
+          {
+            constexpr int NST = NFW * (WS_DR - 2) + SPT * (WS_DR - 1);   // steady state
+            const int n = NFW * mn(WS_DR - 2, t1 - 1 - t) + SPT * mn(WS_DR - 1, t - t0);
+            if (n == NST) vmwait_c<NST>();
+            else vmwait23(n);
+          }
+          const int slot = t % WS_DR;
+          const uint32_t gen = (uint32_t)((t - t0) / WS_DR + 1);
+          flag_signal(&fl_full[slot][wid], gen);   // this wave's DMA of tile t landed
+          flag_wait<WV>(fl_full[slot], gen);       // every wave's
+          mfma_tile(sA[slot], acc);
+          if constexpr (!(CTN_WS_EXP & 64)) __builtin_amdgcn_sched_barrier(0);
+          flag_signal(&fl_done[slot][wid], gen);   // this wave's reads of the slot done
+          const int tn = t + WS_DR - 1;            // into the slot of tile t - 1
+          if (tn < t1) {
+            if (t > t0) flag_wait<WV>(fl_done[(t - 1) % WS_DR], (uint32_t)((t - 1 - t0) / WS_DR + 1));
+            dma(tn);
+          }
+          epilogue_math(le1, t, acc);
+          store_out(t);
+        }
+      } else
       for (int t = t0; t < t1; ++t) {
         {
           constexpr int NST = NFW * (WS_DR - 2) + SPT * (WS_DR - 1);   // steady state
