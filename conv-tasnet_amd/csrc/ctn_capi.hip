@@ -282,7 +282,7 @@ TbLayout tb_layout(const ctn_tblock_desc* d, int backward, void* ws, void* part 
     L.chunks2 = dualA ? gemm_dual_ranges(duA) : gemm_cols_default_chunks(gc);
     L.cpart2 = cp.take<float>((size_t)L.chunks2 * d->B * d->H * sizeof(float));
     gc.P = d->H; gc.Q = d->B;
-    L.chunks1 = dualB ? gemm_dual_ranges(duB) : gemm_cols_default_chunks(gc);
+    L.chunks1 = dualB ? gemm_dual_ranges(duB) : gemm_cols_chunks(dtl, gc);
     L.cpart1 = cp.take<float>((size_t)L.chunks1 * d->B * d->H * sizeof(float));
     const long HB = (long)d->H * d->B, dwb = dw_blocks(da);
     const size_t ntmp = sr_tmp(L.chunks2, HB) + sr_tmp(L.chunks1, HB) + 4 * sr_tmp(dwb, d->H) +
@@ -1550,7 +1550,7 @@ C1Layout c1_layout(const ctn_rows_desc* d, int cout, int bwd, void* ws) {
     if (d->dtype == CTN_DTYPE_BF16) L.ws_w = c.take<void>((size_t)cout * d->C * es);
   } else {
     L.ws_wt = c.take<void>((size_t)cout * d->C * es);
-    L.chunks = gemm_cols_default_chunks(c1_cols(d, cout));
+    L.chunks = gemm_cols_chunks(d->dtype == CTN_DTYPE_BF16 ? BF16 : F32, c1_cols(d, cout));
     L.cpart = c.take<float>((size_t)L.chunks * cout * d->C * sizeof(float));
   }
   L.bytes = c.off + 256;

@@ -181,14 +181,20 @@ CTN_DEV void dv_signal(uint32_t* f, uint32_t gen) {
   asm volatile("" ::: "memory");
 }
 
-template <int NK, int NSL, int PF>
-__global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
+// COLS: the column GEMM alone (ctn_gemm.hip's GemmCols dW = A^T B with plain operands,
+// e.g. dW1 = gh1^T . x): no row waves, op = identity, and the partial stored transposed
+// (Dpart[range][n][k], the GemmCols layout [chunk][P][Q] with P = Nout, Q = Kred) through
+// LDS at the end.  12 waves: column waves 0-7, memory waves 8-11.
+template <int NK, int NSL, int PF, bool COLS = false>
+__global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
+  constexpr int NR = COLS ? 0 : DV_NR;      // row waves
+  constexpr int ND = NR + DV_NC;            // waves that publish DONE
   constexpr int TM = DV_TM, KB = DV_KB, KR = DV_KR, NS = DV_NS;
   constexpr int SLOT = DV_SLOT;
   static_assert(NSL * SLOT <= 160 * 1024 - 2048, "LDS budget");
   __shared__ __attribute__((aligned(16))) char smem[NSL * SLOT];
   __shared__ __attribute__((aligned(16))) uint32_t fl_full[NSL][4];   // per memory wave
-  __shared__ __attribute__((aligned(16))) uint32_t fl_done[NSL][DV_ND];   // per row / column wave
+  __shared__ __attribute__((aligned(16))) uint32_t fl_done[NSL][ND];   // per row / column wave
   __shared__ __attribute__((aligned(16))) float sgb[2][NS];            // gamma2 / beta2 of the slice
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -214,13 +220,27 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
   const int Kp = p.g.Kp, Kv = p.g.K, tpu = Kp / TM;
 
   if (tid < NSL * 4) (&fl_full[0][0])[tid] = 0u;
-  else if (tid < NSL * (4 + DV_ND)) (&fl_done[0][0])[tid - NSL * 4] = 0u;
-  if (tid < 2 * NS) sgb[tid / NS][tid % NS] = (tid < NS ? p.bop.gamma : p.bop.beta)[n0 + tid % NS];
+  else if (tid < NSL * (4 + ND)) (&fl_done[0][0])[tid - NSL * 4] = 0u;
+  if constexpr (!COLS)
+    if (tid < 2 * NS) sgb[tid / NS][tid % NS] = (tid < NS ? p.bop.gamma : p.bop.beta)[n0 + tid % NS];
   __syncthreads();
 
-  const float eal = p.alpha[0];
+  const float eal = COLS ? 0.f : p.alpha[0];
   const int kmax = ws_runs_kmax(ntile, nr, tpu);
-  if (wid < DV_NR) {
+  // COLS: the workgroup's transposed partial [n - n0][k] from the LDS image (COLS_LDT
+  // floats per row) as whole 1-KiB rows of Dpart[range][n][k], by every wave
+  constexpr int COLS_LDT = KR + 4;
+  static_assert(!COLS || NS * COLS_LDT * 4 <= NSL * DV_SLOT, "transpose image fits the ring");
+  static_assert(!COLS || DV_RB, "COLS takes the raw-B slot layout (no operand transform)");
+  auto store_tr = [&](float* Dp) __attribute__((always_inline)) {
+    const float* img = reinterpret_cast<const float*>(smem);
+    for (int idx = tid; idx < NS * (KR / 4); idx += (DV_NC + DV_NMW) * 64) {
+      const int nl = idx / (KR / 4), k4 = idx % (KR / 4);
+      *reinterpret_cast<float4*>(Dp + (size_t)(n0 + nl) * KR + 4 * k4) =
+          *reinterpret_cast<const float4*>(img + nl * COLS_LDT + 4 * k4);
+    }
+  };
+  if (wid < NR) {
     // ======================= row waves =======================
     // wave r: output channels n0 + 32r .. +31 of both 16-row blocks of every tile, against
     // the resident W fragments (group 4*sl + r of the fragment-ordered copy, nb = 0, 1):
@@ -367,12 +387,12 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
     }
     return;
   }
-  if (wid < DV_NR + DV_NC) {
+  if (wid < ND) {
     // ======================= column waves =======================
     // wave c = (wp, wn) owns dW2 blocks p in [16 CI wp, +16 CI), n in [n0 + 16 CJ wn, +16 CJ):
     // dW2 += gy_tile^T . op(d)_tile, the reduction over the tile's 32 frame rows
     constexpr int CI = DV_CI, CJ = DV_CJ;
-    const int c = wid - DV_NR, wp = c / (8 / CJ), wn = c % (8 / CJ);
+    const int c = wid - NR, wp = c / (8 / CJ), wn = c % (8 / CJ);
     f32x4_t dacc[CI][CJ];
 #pragma unroll
     for (int i = 0; i < CI; ++i)
@@ -395,10 +415,10 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
     float cg[CJ], cb[CJ];
 #pragma unroll
     for (int j = 0; j < CJ; ++j) {
-      cg[j] = sgb[0][16 * (CJ * wn + j) + lr];
-      cb[j] = sgb[1][16 * (CJ * wn + j) + lr];
+      cg[j] = COLS ? 0.f : sgb[0][16 * (CJ * wn + j) + lr];
+      cb[j] = COLS ? 0.f : sgb[1][16 * (CJ * wn + j) + lr];
     }
-    const float bal = p.bop.alpha[0];
+    const float bal = COLS ? 0.f : p.bop.alpha[0];
     auto run = [&](auto le1) __attribute__((always_inline)) {
       constexpr bool LE1 = decltype(le1)::value;
       int slot = 0;
@@ -416,7 +436,7 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
             const s16x4_t hi = dv_tr(bb + (DV_RB ? bbase[1] ^ (j << 5) : bbase[1] + j * DV_BST));
             bfr[j] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
           }
-          if constexpr (DV_RB) {
+          if constexpr (DV_RB && !COLS) {
             float mu[8], rs[8];
             if constexpr (NK == NORM_GLN) {
               const float2 st = *reinterpret_cast<const float2*>(base + OFF_ST);
@@ -458,17 +478,34 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
             for (int j = 0; j < CJ; ++j) dacc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], dacc[i][j], 0, 0, 0);
           }
         }
-        dv_signal(&fl_done[slot][DV_NR + c], gen);
+        dv_signal(&fl_done[slot][NR + c], gen);
         if (++slot == NSL) {
           slot = 0;
           ++gen;
         }
       }
     };
-    if (bal <= 1.f) run(std::true_type{});
+    if (COLS || bal <= 1.f) run(std::true_type{});
     else run(std::false_type{});
     // dW2 partial of this workgroup: lane holds D[(wp*CI+i)*16 + 4lg + e][n0 + (wn*CJ+j)*16 + lr]
     float* Dp = p.Dpart + (size_t)rr * KR * p.Nout;
+    if constexpr (COLS) {
+      // transposed through LDS (the ring is idle once every wave is past the barrier):
+      // image [n - n0][k] fp32, rows padded by 4 floats against bank conflicts
+      float* img = reinterpret_cast<float*>(smem);
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < CI; ++i)
+#pragma unroll
+        for (int j = 0; j < CJ; ++j) {
+          const int nl = (wn * CJ + j) * 16 + lr;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) img[nl * COLS_LDT + (wp * CI + i) * 16 + 4 * lg + e] = dacc[i][j][e];
+        }
+      __syncthreads();
+      store_tr(Dp);
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < CI; ++i)
 #pragma unroll
@@ -489,7 +526,7 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
   // and publishes FULL.  A slot is refilled only after every row / column wave's DONE for
   // the tile that used it last.  RAWB=1: the raw-d pieces land in the B image itself and
   // wave 0 alone fetches the tile's statistics (all 32 rows).
-  const int mw = wid - DV_ND;
+  const int mw = wid - ND;
   const rsrc_t rA = du_rsrc(p.A, rows * p.lda * 2), rD = du_rsrc(p.Bm, rows * p.ldb * 2);
   const rsrc_t rS = du_rsrc(p.bop.stats, (NK == NORM_GLN ? (long)p.g.M : rows) * 8);
   int arow[4];
@@ -519,8 +556,8 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
   // cLN rows 8m .. 8m+7 (lanes 0..15), gLN the pair.  Other lanes read out of range (zeros).
   const bool st_lane = NK == NORM_CLN ? (DV_RB ? true : lane < 16) : lane < 2;
   const uint32_t soff = st_lane ? (uint32_t)((NK == NORM_CLN && !DV_RB ? 8 * mw * 8 : 0) + lane * 4) : DU_OOB;
-  const bool st_wave = !DV_RB || mw == 0;
-  const float bal = p.bop.alpha[0];
+  const bool st_wave = !COLS && (!DV_RB || mw == 0);
+  const float bal = COLS ? 0.f : p.bop.alpha[0];
   // DMA instructions per wave and tile: 7 (st_wave), else 6 (RAWB=1 waves 1..3)
 
   auto dma = [&](int t) __attribute__((always_inline)) {
@@ -587,7 +624,7 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
       const int tn = t + PF;
       if (tn < t1) {
         const int kn = tn - t0;   // its slot was last used by tile tn - NSL: wait for every DONE of it
-        dv_wait<DV_ND>(fl_done[kn % NSL], (uint32_t)(kn / NSL));
+        dv_wait<ND>(fl_done[kn % NSL], (uint32_t)(kn / NSL));
         dma(tn);
       }
       if (++slot == NSL) {
@@ -598,8 +635,13 @@ __global__ __launch_bounds__(DV_NT) void gemm_dual_ws_kernel(GemmDual p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may land after the wave ends
   };
   if (t0 < t1) {
-    if (bal <= 1.f) run(std::true_type{});
+    if (COLS || bal <= 1.f) run(std::true_type{});
     else run(std::false_type{});
+  }
+  if constexpr (COLS) {   // the column waves' two barriers, then a share of the stores
+    __syncthreads();
+    __syncthreads();
+    store_tr(p.Dpart + (size_t)rr * KR * p.Nout);
   }
 }
 
@@ -630,6 +672,40 @@ int gemm_dual_ws_ranges(const GemmDual& p) {
   const long nt = p.g.rows() / DV_TM;
   const int want = DV_GRID / (p.Nout / DV_NS);
   return (int)(nt < want ? nt : want);
+}
+
+// The column GEMM alone (GemmCols, plain bf16 operands): dW[P][Q] partials per row range
+// = A^T B with A [rows][P] (P = Nout, sliced by 128 per workgroup) and B [rows][Q]
+// (Q = Kred = 256, whole rows), i.e. the dual's column part with the roles of its
+// operands swapped: its "A" tile is B and its raw-B slice is A.
+bool gemm_cols_ws_eligible(DType dt, const GemmCols& c) {
+  const char* e = getenv("CTN_COLS_WS");
+  if (e && atoi(e) == 0) return false;
+  if (dt != BF16 || c.aop.kind != OP_PLAIN || c.bop.kind != OP_PLAIN) return false;
+  if (c.Q != DV_KR || c.P % DV_NS || DV_GRID % (c.P / DV_NS)) return false;
+  if (c.g.Kp % DV_TM || c.lda % 8 || c.ldb % 8 || c.g.rows() / DV_TM < 1) return false;
+  if (((uintptr_t)c.A | (uintptr_t)c.B | (uintptr_t)c.Cpart) & 15) return false;
+  return true;
+}
+
+int gemm_cols_ws_ranges(const GemmCols& c) {
+  const long nt = c.g.rows() / DV_TM;
+  const int want = DV_GRID / (c.P / DV_NS);
+  return (int)(nt < want ? nt : want);
+}
+
+hipError_t launch_gemm_cols_ws(const GemmCols& c, hipStream_t s) {
+  GemmDual p{};
+  p.g = c.g;
+  p.Kred = c.Q;
+  p.Nout = c.P;
+  p.A = c.B; p.lda = c.ldb;     // whole 256-channel rows: the fragment-order tile
+  p.Bm = c.A; p.ldb = c.lda;    // the 128-channel slice: raw B
+  p.Dpart = c.Cpart;            // [range][P][Q]
+  const dim3 grid(gemm_cols_ws_ranges(c) * (c.P / DV_NS));
+  hipLaunchKernelGGL((gemm_dual_ws_kernel<NORM_GLN, DV_NSL, DV_NSL - 1, true>), grid, dim3((DV_NC + DV_NMW) * 64), 0,
+                     s, p);
+  return hipGetLastError();
 }
 
 hipError_t launch_gemm_dual_ws(const GemmDual& p, hipStream_t s) {

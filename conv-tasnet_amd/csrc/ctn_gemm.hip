@@ -746,7 +746,14 @@ static hipError_t dispatch_cols_nk(const GemmCols& p, hipStream_t s) {
   return hipErrorInvalidValue;
 }
 
+// Partial count of a column GEMM as launch_gemm_cols will run it: the wave-specialised
+// kernel's row ranges where it applies (ctn_dual_ws.hip), else the tiled kernel's chunks.
+int gemm_cols_chunks(DType dt, const GemmCols& p) {
+  return gemm_cols_ws_eligible(dt, p) ? gemm_cols_ws_ranges(p) : gemm_cols_default_chunks(p);
+}
+
 hipError_t launch_gemm_cols(DType dt, const GemmCols& p, hipStream_t s) {
+  if (gemm_cols_ws_eligible(dt, p) && p.nchunks == gemm_cols_ws_ranges(p)) return launch_gemm_cols_ws(p, s);
   if (p.g.Kp % CKR != 0 || p.P % 8 != 0 || p.Q % 8 != 0 || p.nchunks < 1 || p.g.rows() >= (1L << 31))
     return hipErrorInvalidValue;
   const int nk = p.bop.kind != OP_PLAIN ? p.bop.norm : 0;

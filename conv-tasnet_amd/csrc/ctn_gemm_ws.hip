@@ -45,13 +45,14 @@ constexpr int WS_WAVES = 8, WS_TM = 16, WS_GRID = CTN_WS_GRID;
 #define CTN_WS_DR 4
 #endif
 constexpr int WS_DR = CTN_WS_DR;
-// The LDS-DMA ring's hand-offs (gLN, no in-kernel cLN finalize): 1 (default) = generation
-// words per slot and wave instead of one workgroup barrier per tile — a wave starts tile
-// t's MFMAs once every wave's DMA of tile t has landed and refills a slot once every wave
-// has read it, so the waves drift within the ring (one wave's epilogue beside another's
-// MFMAs) instead of running MFMA, VALU and stores in lockstep.
+// The LDS-DMA ring's hand-offs (gLN, no in-kernel cLN finalize): 1 = generation words per
+// slot and wave instead of one workgroup barrier per tile — a wave starts tile t's MFMAs
+// once every wave's DMA of tile t has landed and refills a slot once every wave has read
+// it, so the waves may drift within the ring.  Measured slower (forward 1x1 35.4 ->
+// 40.6 / 41.7 / 43.0 us at rings of 4 / 6 / 8 tiles): 0 (default) keeps the
+// barrier.
 #ifndef CTN_WS_FLAGS
-#define CTN_WS_FLAGS 1
+#define CTN_WS_FLAGS 0
 #endif
 constexpr int WS_FOLD_MAX = 512;   // utterances whose gLN operand stats a workgroup holds in LDS
 

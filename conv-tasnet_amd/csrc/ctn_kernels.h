@@ -124,6 +124,12 @@ bool gemm_dual_ws_enabled();
 bool gemm_dual_ws_eligible(const GemmDual& p);
 int gemm_dual_ws_ranges(const GemmDual& p);
 hipError_t launch_gemm_dual_ws(const GemmDual& p, hipStream_t s);
+// the same kernel's column part alone for plain bf16 column GEMMs (dW1 = gh1^T . x):
+// chosen by launch_gemm_cols when nchunks == gemm_cols_ws_ranges (gemm_cols_chunks)
+bool gemm_cols_ws_eligible(DType dt, const GemmCols& c);
+int gemm_cols_ws_ranges(const GemmCols& c);
+hipError_t launch_gemm_cols_ws(const GemmCols& c, hipStream_t s);
+int gemm_cols_chunks(DType dt, const GemmCols& c);   // partial count the launch will use
 
 // ---- statistics ------------------------------------------------------------
 // slab: [G][nparts] double2 partials -> out[G] float2
