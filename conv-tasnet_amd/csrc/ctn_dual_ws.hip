@@ -71,6 +71,12 @@ constexpr int DV_NSL = CTN_DV_NSL;               // LDS ring slots (NSL - 1 tile
 #endif
 constexpr int DV_CJ = CTN_DV_CJ, DV_CI = 16 / DV_CJ;
 static_assert(DV_CJ == 1 || DV_CJ == 2 || DV_CJ == 4, "column blocks per column wave");
+// COLS mode (no operand transform to share): the split that reads the fewest fragments
+#ifndef CTN_DV_CJC
+#define CTN_DV_CJC 4
+#endif
+constexpr int DV_CJC = CTN_DV_CJC;
+static_assert(DV_CJC == 1 || DV_CJC == 2 || DV_CJC == 4, "column blocks per column wave (COLS)");
 
 // Row waves: A fragments read LA k-steps ahead of their MFMAs
 #ifndef CTN_DV_LA
@@ -391,7 +397,7 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
     // ======================= column waves =======================
     // wave c = (wp, wn) owns dW2 blocks p in [16 CI wp, +16 CI), n in [n0 + 16 CJ wn, +16 CJ):
     // dW2 += gy_tile^T . op(d)_tile, the reduction over the tile's 32 frame rows
-    constexpr int CI = DV_CI, CJ = DV_CJ;
+    constexpr int CJ = COLS ? DV_CJC : DV_CJ, CI = 16 / CJ;
     const int c = wid - NR, wp = c / (8 / CJ), wn = c % (8 / CJ);
     f32x4_t dacc[CI][CJ];
 #pragma unroll

@@ -420,8 +420,17 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
     for (int i = 0; i < 4; ++i) ah[i] = (pr2(f32x2_t{rh[2 * i], rh[2 * i + 1]}, al1) + nm) * st.y;
   };
 
-  f32x2_t gdw[P][4], ahw[P][4];
-  bool ahok[P];
+  // nw: the depthwise-weight gradient's operand of each window row, n1 = gamma1 * hat a1 +
+  // beta1 (0 for rows outside the utterance), formed once when the row enters the window
+  // instead of at each of its P uses
+  f32x2_t gdw[P][4], ahw[P][4], nw[P][4];
+  auto enter_n = [&](int q, bool ok) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const f32x2_t n = pfma(ahw[q][i], g1[i], b1[i]);
+      nw[q][i] = f32x2_t{ok ? n[0] : 0.f, ok ? n[1] : 0.f};
+    }
+  };
 #pragma unroll
   for (int i = 0; i < P - 1; ++i) {
     Raw8<T> rd, rg, rh; bool ok, okh; int row, rowh;
@@ -430,7 +439,7 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
     fetch_h(it.j0 + AT - P + 1 + i, rh, okh, rowh);
     finish_g(rd, rg, ok, row, sg >= it.j0 && sg < it.j1, gdw[i]);   // alpha2 term: own rows only
     finish_h(rh, rowh, ahw[i]);
-    ahok[i] = okh;
+    enter_n(i, okh);
   }
   constexpr int D = dw_pf<T>();   // rows in flight per lane, slots as in dw_fwd
   const bool wave_item = gm.cg == 64;   // one comb item per wave (see RowPark)
@@ -452,7 +461,7 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
                   int crowh) __attribute__((always_inline)) {
     finish_g(cd, cgv, cok, crow, j + GT < it.j1, gdw[P - 1]);   // halo rows are counted by their own segment
     finish_h(ch, crowh, ahw[P - 1]);
-    ahok[P - 1] = cokh;
+    enter_n(P - 1, cokh);
     const int k = row_of(j);
     f32x2_t ga1[4] = {z2, z2, z2, z2};
     float s = 0.f, ss = 0.f;
@@ -465,12 +474,9 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
         for (int q = 1; q < P; ++q) gn1[i] = pfma(w[q][i], gdw[P - 1 - q][i], gn1[i]);
       }
 #pragma unroll
-      for (int q = 0; q < P; ++q) {
-        const float okq = ahok[q] ? 1.f : 0.f;   // window rows outside the utterance add 0
+      for (int q = 0; q < P; ++q)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          cwd[q][i] = pfma(gdw[P - 1 - POWN][i] * okq, pfma(ahw[q][i], g1[i], b1[i]), cwd[q][i]);
-      }
+        for (int i = 0; i < 4; ++i) cwd[q][i] = pfma(gdw[P - 1 - POWN][i], nw[q][i], cwd[q][i]);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const f32x2_t ah = ahw[POWN][i];
@@ -511,14 +517,13 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwArgs a) {
       }
     }
 #pragma unroll
-    for (int i = 0; i < P - 1; ++i) {
-      ahok[i] = ahok[i + 1];
+    for (int i = 0; i < P - 1; ++i)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         gdw[i][e] = gdw[i + 1][e];
         ahw[i][e] = ahw[i + 1][e];
+        nw[i][e] = nw[i + 1][e];
       }
-    }
   };
   Raw8<T> pd[D], pg[D], ph[D]; bool pok[D], pokh[D]; int prow[D], prowh[D];
 #pragma unroll

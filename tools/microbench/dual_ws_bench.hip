@@ -214,5 +214,26 @@ int main(int argc, char** argv) {
     printf("EXP %d %-4s M=%d K=%d %s %8.1f us  %7.0f GB/s (alg. bytes)\n", CTN_DV_EXP, ws ? "ws" : "old", M, K,
            NK == NORM_GLN ? "gLN" : "cLN", us, bytes / us * 1e-3);
   }
+  // the same kernel's COLS mode (dW1 = gh1^T . x shape: A = d [rows][H], B = gy [rows][B])
+  {
+    GemmCols c{};
+    c.g = g.g; c.P = H; c.Q = B;
+    c.A = d; c.lda = H; c.B = gy; c.ldb = B;
+    c.nchunks = gemm_cols_ws_ranges(c);
+    float* cp; CK(hipMalloc(&cp, (size_t)c.nchunks * H * B * 4));
+    c.Cpart = cp;
+    if (gemm_cols_ws_eligible(BF16, c)) {
+      for (int i = 0; i < 3; ++i) CK(launch_gemm_cols_ws(c, 0));
+      CK(hipDeviceSynchronize());
+      CK(hipEventRecord(e0, 0));
+      for (int i = 0; i < NIT; ++i) CK(launch_gemm_cols_ws(c, 0));
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+      const double us = ms * 1e3 / NIT, cb = rows * (B + H) * 2.0;
+      printf("COLS CJC=%d M=%d K=%d %8.1f us  %7.0f GB/s (alg. bytes, %d ranges)\n", CTN_DV_CJC, M, K, us, cb / us * 1e-3,
+             c.nchunks);
+    }
+  }
   return 0;
 }
