@@ -266,20 +266,23 @@ class TemporalBlock(nn.Module):
         if stride != 1:
             raise ValueError("TemporalBlock: only stride 1 is used by the reference (conv_tasnet.py:177)")
 
+    # Sub-modules by their Sequential keys (dict lookups: this runs for every block on
+    # every step, and nn.Sequential indexing goes through islice)
     def _norms(self):
-        ds = self.net[3].net
-        return self.net[2], ds[3 if self._geo[4] else 2]
+        m = self.net._modules
+        return m['2'], m['3'].net._modules['3' if self._geo[4] else '2']
 
     def _params(self):
-        ds = self.net[3].net
+        m = self.net._modules
+        ds = m['3'].net._modules
         off = 1 if self._geo[4] else 0
-        n1, n2 = self._norms()
+        n1, n2 = m['2'], ds[str(2 + off)]
         if isinstance(n1, nn.BatchNorm1d):
             g1, b1, g2, b2 = n1.weight, n1.bias, n2.weight, n2.bias
         else:
             g1, b1, g2, b2 = n1.gamma, n1.beta, n2.gamma, n2.beta
-        return (self.net[0].weight, self.net[1].weight, g1, b1, ds[0].weight,
-                ds[1 + off].weight, g2, b2, ds[3 + off].weight)
+        return (m['0'].weight, m['1'].weight, g1, b1, ds['0'].weight,
+                ds[str(1 + off)].weight, g2, b2, ds[str(3 + off)].weight)
 
     def _forward_rows(self, x_rows, fr, norm, pack=None, wgrad_split=False, defer=False):
         B, H, P, dil, causal, _ = self._geo
