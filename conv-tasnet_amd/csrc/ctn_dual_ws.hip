@@ -684,9 +684,12 @@ int gemm_dual_ws_ranges(const GemmDual& p) {
 // = A^T B with A [rows][P] (P = Nout, sliced by 128 per workgroup) and B [rows][Q]
 // (Q = Kred = 256, whole rows), i.e. the dual's column part with the roles of its
 // operands swapped: its "A" tile is B and its raw-B slice is A.
+// Off by default (CTN_COLS_WS=1 to enable): 47.8 us against the tiled kernel's 49.4 in the
+// step, but twice the partial bytes (64 row ranges instead of 32 chunks) cost the slab
+// reduction more than that: bench 2129 vs 2142 utt/s.
 bool gemm_cols_ws_eligible(DType dt, const GemmCols& c) {
   const char* e = getenv("CTN_COLS_WS");
-  if (e && atoi(e) == 0) return false;
+  if (!e || atoi(e) == 0) return false;
   if (dt != BF16 || c.aop.kind != OP_PLAIN || c.bop.kind != OP_PLAIN) return false;
   if (c.Q != DV_KR || c.P % DV_NS || DV_GRID % (c.P / DV_NS)) return false;
   if (c.g.Kp % DV_TM || c.lda % 8 || c.ldb % 8 || c.g.rows() / DV_TM < 1) return false;

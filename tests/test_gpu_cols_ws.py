@@ -1,6 +1,6 @@
 """The wave-specialised column GEMM (ctn_dual_ws.hip, COLS mode: memory + column waves
-only, plain bf16 operands, transposed partials) that computes the first 1x1 conv's
-weight gradient dW1 = gh1^T . x in the block backward, checked through the public 1x1
+only, plain bf16 operands, transposed partials; opt-in, CTN_COLS_WS=1) that can compute
+the first 1x1 conv's weight gradient dW1 = gh1^T . x in the block backward, checked through the public 1x1
 conv layer (ctn_conv1x1_backward: dW = gy^T . x, the same GemmCols shape C=256 -> 512):
 against an fp32 matmul of the same bf16 operands, against the tiled column kernel
 (CTN_COLS_WS=0), and run to run bitwise.  Padded frame rows contribute nothing.  GPU
