@@ -27,14 +27,16 @@ import streaming  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
+    ap.add_argument("--streams", default="1,16,64", help="comma-separated stream counts")
+    ap.add_argument("--frames", default="1,4,16,64", help="comma-separated chunk sizes in frames")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     model = ct.ConvTasNet(256, 16, 256, 512, 3, 8, 4, 2, norm_type="cLN", causal=True).to(dev).eval()
     rate, stride = 16000, 8
     rows = []
-    for M in (1, 16, 64):
-        for F in (1, 4, 16, 64):
+    for M in [int(v) for v in args.streams.split(",")]:
+        for F in [int(v) for v in args.frames.split(",")]:
             s = streaming.StreamingSeparator(model)
             n = F * stride
             x = torch.randn(M, n * 70 + 16, device=dev)
