@@ -1,3 +1,4 @@
+#include <stdlib.h>
 // Streaming causal separation (gfx950): a causal cLN (or eval-mode BatchNorm)
 // Conv-TasNet run frame group by frame group with per-block state, no history
 // re-run (src/separate.py:35-79 with a causal model; conv_tasnet.py:176, 289).
@@ -298,16 +299,19 @@ __global__ __launch_bounds__(ST_NT) void stream_ola_kernel(StreamArgs a) {
 //   SD1 mask 1x1 chunk (all speakers of 32 channels), nonlinearity, * w -> sources
 //   SD2 sources . V^T -> frames, overlap-add with the carried tail
 // ===========================================================================
-constexpr int SC_W = 32;                 // outputs per chunk workgroup
-constexpr int SC_SL = ST_NT / SC_W;      // input slices per output (8)
+// outputs per chunk workgroup: SC_W = 32 (8 input slices per output) for calls with many
+// frames x streams, 8 (32 slices) for small calls, where a kernel's few workgroups each
+// streaming a 32-column weight slice left the call latency-bound (14.5 us per block
+// kernel at 1 stream x 1 frame); chosen per launch (sc_width)
 constexpr int SC_FPB = 8;                // frames per workgroup (SE, SA, SD1)
 
 // res[f] (valid in threads t < SC_W) = sum_i Wt[i][j0 + t] * in[f][i]; thread (o, s) sums
 // the inputs i = s, s + 8, ... (a 128-byte weight row segment per 32 threads), then the
 // 8 slices are added in order.  red: SC_FPB * ST_NT floats.
-template <int F>
+template <int F, int SC_W>
 CTN_DEV void sc_matvec(const float* __restrict__ Wt, int n_in, int n_out, int j0, const float* in, int ld_in, int nf,
                        float (&res)[F], float* red) {
+  constexpr int SC_SL = ST_NT / SC_W;   // input slices per output
   const int t = threadIdx.x, o = t % SC_W, sl = t / SC_W, j = j0 + o;
   float acc[F];
 #pragma unroll
@@ -336,6 +340,7 @@ CTN_DEV void sc_matvec(const float* __restrict__ Wt, int n_in, int n_out, int j0
   __syncthreads();
 }
 
+template <int SC_W>
 __global__ __launch_bounds__(ST_NT) void sc_encode_kernel(StreamArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int N = a.N, L = a.L, S = a.L / 2, Bc = a.B;
@@ -357,11 +362,12 @@ __global__ __launch_bounds__(ST_NT) void sc_encode_kernel(StreamArgs a) {
   __syncthreads();
   st_norm_rows<SC_FPB>(y, N, nf, N, 1, a.na, a.nb, red);   // separator cLN (always channel-wise)
   float res[SC_FPB];
-  sc_matvec<SC_FPB>(a.W, N, Bc, j0, y, N, nf, res, red);
+  sc_matvec<SC_FPB, SC_W>(a.W, N, Bc, j0, y, N, nf, res, red);
   if (threadIdx.x < SC_W && j0 + (int)threadIdx.x < Bc)
     for (int f = 0; f < nf; ++f) a.x_out[((size_t)m * a.K + f0 + f) * Bc + j0 + threadIdx.x] = res[f];
 }
 
+template <int SC_W>
 __global__ __launch_bounds__(ST_NT) void sc_block_in_kernel(StreamArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int Bc = a.B, H = a.H;
@@ -371,11 +377,12 @@ __global__ __launch_bounds__(ST_NT) void sc_block_in_kernel(StreamArgs a) {
   for (int i = threadIdx.x; i < nf * Bc; i += ST_NT) xs[i] = a.x_in[((size_t)m * a.K + f0) * Bc + i];
   __syncthreads();
   float res[SC_FPB];
-  sc_matvec<SC_FPB>(a.W, Bc, H, j0, xs, Bc, nf, res, red);
+  sc_matvec<SC_FPB, SC_W>(a.W, Bc, H, j0, xs, Bc, nf, res, red);
   if (threadIdx.x < SC_W && j0 + (int)threadIdx.x < H)
     for (int f = 0; f < nf; ++f) a.frames[((size_t)m * a.K + f0 + f) * H + j0 + threadIdx.x] = res[f];   // h1 scratch
 }
 
+template <int SC_W>
 __global__ __launch_bounds__(ST_NT) void sc_block_out_kernel(StreamArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int Bc = a.B, H = a.H, P = a.P, dil = a.dil;
@@ -416,7 +423,7 @@ __global__ __launch_bounds__(ST_NT) void sc_block_out_kernel(StreamArgs a) {
   __syncthreads();
   st_norm_rows<1>(d, H, 1, H, a.norm, a.na2, a.nb2, red);
   float res[1];
-  sc_matvec<1>(a.W2, H, Bc, j0, d, H, 1, res, red);
+  sc_matvec<1, SC_W>(a.W2, H, Bc, j0, d, H, 1, res, red);
   if (threadIdx.x < SC_W && j0 + (int)threadIdx.x < Bc) {
     const size_t o = ((size_t)m * a.K + f) * Bc + j0 + threadIdx.x;
     a.x_out[o] = res[0] + a.x_in[o];                         // + residual
@@ -425,6 +432,7 @@ __global__ __launch_bounds__(ST_NT) void sc_block_out_kernel(StreamArgs a) {
 
 // sources[m][c][k][n] = w * mask: the mask 1x1 for all speakers of 32 channels n, then
 // the nonlinearity across speakers (conv_tasnet.py:185, 202-207, 137)
+template <int SC_W>
 __global__ __launch_bounds__(ST_NT) void sc_decode_mask_kernel(StreamArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int Bc = a.B, N = a.N, C = a.C, CN = C * N;
@@ -436,7 +444,7 @@ __global__ __launch_bounds__(ST_NT) void sc_decode_mask_kernel(StreamArgs a) {
   __syncthreads();
   for (int c = 0; c < C; ++c) {
     float res[SC_FPB];
-    sc_matvec<SC_FPB>(a.W, Bc, CN, c * N + n0, xs, Bc, nf, res, red);
+    sc_matvec<SC_FPB, SC_W>(a.W, Bc, CN, c * N + n0, xs, Bc, nf, res, red);
     if (threadIdx.x < SC_W)
       for (int f = 0; f < SC_FPB; ++f) sc[(c * SC_FPB + f) * SC_W + threadIdx.x] = res[f];
   }
@@ -490,7 +498,7 @@ size_t stream_call_smem(int which, const StreamArgs& a) {
     case 0: return (size_t)(((SC_FPB - 1) * S + a.L + 3) / 4 * 4 + SC_FPB * a.N + SC_FPB * ST_NT) * 4;
     case 1: return (size_t)(SC_FPB * a.B + SC_FPB * ST_NT) * 4;
     case 2: return (size_t)(a.P * a.H + a.H + SC_FPB * ST_NT) * 4;
-    case 3: return (size_t)(SC_FPB * a.B + a.C * SC_FPB * SC_W + SC_FPB * ST_NT) * 4;
+    case 3: return (size_t)(SC_FPB * a.B + a.C * SC_FPB * 32 + SC_FPB * ST_NT) * 4;   // SC_W <= 32
     default: return (size_t)a.K * a.L * 4;
   }
 }
@@ -504,20 +512,33 @@ hipError_t launch_stream_set_pos(long* pos_dev, long pos, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_stream_call_stage(int which, const StreamArgs& a, hipStream_t s) {
-  const size_t lds = stream_call_smem(which, a);
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
+template <int SC_W>
+static hipError_t sc_launch(int which, const StreamArgs& a, size_t lds, hipStream_t s) {
   const unsigned fg = (unsigned)((a.K + SC_FPB - 1) / SC_FPB);
   const dim3 b(ST_NT);
   switch (which) {
-    case 0: hipLaunchKernelGGL(sc_encode_kernel, dim3(a.M, fg, (a.B + SC_W - 1) / SC_W), b, lds, s, a); break;
-    case 1: hipLaunchKernelGGL(sc_block_in_kernel, dim3(a.M, fg, (a.H + SC_W - 1) / SC_W), b, lds, s, a); break;
-    case 2: hipLaunchKernelGGL(sc_block_out_kernel, dim3(a.M, a.K, (a.B + SC_W - 1) / SC_W), b, lds, s, a); break;
-    case 3: hipLaunchKernelGGL(sc_decode_mask_kernel, dim3(a.M, fg, (a.N + SC_W - 1) / SC_W), b, lds, s, a); break;
+    case 0: hipLaunchKernelGGL(sc_encode_kernel<SC_W>, dim3(a.M, fg, (a.B + SC_W - 1) / SC_W), b, lds, s, a); break;
+    case 1: hipLaunchKernelGGL(sc_block_in_kernel<SC_W>, dim3(a.M, fg, (a.H + SC_W - 1) / SC_W), b, lds, s, a); break;
+    case 2: hipLaunchKernelGGL(sc_block_out_kernel<SC_W>, dim3(a.M, a.K, (a.B + SC_W - 1) / SC_W), b, lds, s, a); break;
+    case 3: hipLaunchKernelGGL(sc_decode_mask_kernel<SC_W>, dim3(a.M, fg, (a.N + SC_W - 1) / SC_W), b, lds, s, a); break;
     case 4: hipLaunchKernelGGL(sc_decode_ola_kernel, dim3(a.M * a.C), b, lds, s, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+// narrow chunks while the (stream, frame) work units of a call are few (CTN_SC_W=8|32
+// forces one width)
+static int sc_width(const StreamArgs& a) {
+  const char* e = getenv("CTN_SC_W");
+  if (e) return atoi(e) == 8 ? 8 : 32;
+  return (long)a.M * a.K < 64 ? 8 : 32;
+}
+
+hipError_t launch_stream_call_stage(int which, const StreamArgs& a, hipStream_t s) {
+  const size_t lds = stream_call_smem(which, a);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  return sc_width(a) == 8 ? sc_launch<8>(which, a, lds, s) : sc_launch<32>(which, a, lds, s);
 }
 
 size_t stream_smem(int which, const StreamArgs& a) {
