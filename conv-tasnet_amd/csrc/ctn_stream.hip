@@ -527,12 +527,12 @@ static hipError_t sc_launch(int which, const StreamArgs& a, size_t lds, hipStrea
   return hipGetLastError();
 }
 
-// narrow chunks while the (stream, frame) work units of a call are few (CTN_SC_W=8|32
+// narrow chunks while the (stream, frame) work units of a call are few (<= 128; CTN_SC_W=8|32
 // forces one width)
 static int sc_width(const StreamArgs& a) {
   const char* e = getenv("CTN_SC_W");
   if (e) return atoi(e) == 8 ? 8 : 32;
-  return (long)a.M * a.K < 64 ? 8 : 32;
+  return (long)a.M * a.K <= 128 ? 8 : 32;
 }
 
 hipError_t launch_stream_call_stage(int which, const StreamArgs& a, hipStream_t s) {
