@@ -15,4 +15,4 @@ for grp in "SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES
   echo "PASS $i ($grp) EXIT $rc"
   [ $rc -eq 0 ] || { tail -5 $OUT/p$i.log; exit 1; }
 done
-python3 tools/pmc_mfma.py $OUT > $OUT/summary.txt && cat $OUT/summary.txt
+python3 tools/pmc_mfma.py $OUT $OUT/pmc_mfma.json > $OUT/summary.txt && cat $OUT/summary.txt

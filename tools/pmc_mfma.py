@@ -12,7 +12,7 @@ json_out = sys.argv[2] if len(sys.argv) > 2 else None
 KINDS = {   # bench.py timer kinds -> kernel name (bf16 throughput mode)
     "1": "gemm_ws_kernel<0, 0, 1, 2, 8, 16, 2, 1>",
     "2": "dw_fwd_kernel<unsigned short, 0, 3, false>",
-    "3": "gemm_dual_kernel<8, 8, 2, 3, 2, 0, 4>",
+    "3": "(anonymous namespace)::gemm_dual_ws_kernel<0, 6, 5, false>",   # the wave-specialised pair-A dual
 }
 vals = defaultdict(lambda: defaultdict(list))
 for f in sorted(glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)):
