@@ -50,7 +50,7 @@ def test_pmc_step_sums_one_steady_step(tmp_path):
 
 def test_pmc_traffic_per_launch(tmp_path):
     pmc = tmp_path / "pmc"
-    name = "void ctn::gemm_dual_kernel<8, 8, 2, 3, 2, 0, 4>(ctn::GemmDual)"
+    name = "void ctn::(anonymous namespace)::gemm_dual_ws_kernel<0, 6, 5, false>(ctn::GemmDual)"
     _counters(str(pmc), {name: (1000.0, 400.0, 2)})
     out = tmp_path / "t.json"
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"), str(pmc), str(out)], check=True,
