@@ -220,6 +220,15 @@ GemmRows tb_gemmB(const ctn_tblock_desc* d, bool fused) {
 // norm1_bwd_kernel.
 // CTN_FUSE_N1=0 keeps the separate kernel (read on every query, so a process can
 // compare both paths: tests/test_gpu_tblock.py).
+// gLN statistics of the weight-stationary GEMMs' operands: folded from the producer's
+// partials in every workgroup's prologue (default) or finalized by a separate launch
+// before them (A/B; read on every call).  bit 0: the output 1x1 GEMM (norm 2 from dw_fwd),
+// bit 1: the gx GEMM (norm-1 backward sums from dw_bwd).
+static int ws_fold_mask() {
+  const char* e = getenv("CTN_WS_FOLD");
+  return e ? atoi(e) : 3;
+}
+
 bool tb_fused_n1(const ctn_tblock_desc* d) {
   const char* e = getenv("CTN_FUSE_N1");
   if (e && atoi(e) == 0) return false;
@@ -633,7 +642,8 @@ extern "C" int ctn_tblock_forward(const ctn_tblock_desc* d, const ctn_tblock_par
   g2.W = w2; g2.ldw = d->H; g2.Wf = w2f;
   g2.epi = EPI_RESID; g2.R = x; g2.ldr = d->B;
   g2.C = y; g2.ldc = d->B;
-  if (fold && gemm_ws_can_fold(dt, g2)) g2.aop.fold = StatFold{L.slab2, L.parts2, cnt, (float)kEps, 0, st2};
+  if (fold && (ws_fold_mask() & 1) && gemm_ws_can_fold(dt, g2))
+    g2.aop.fold = StatFold{L.slab2, L.parts2, cnt, (float)kEps, 0, st2};
   else if (!da.st2_out) CTN_HIP(launch_stats_finalize(L.slab2, G, L.parts2, cnt, 0, (float)kEps, st2, s));
   CTN_HIP(launch_gemm_rows(dt, g2, s));
   return CTN_OK;
@@ -796,8 +806,12 @@ static int tb_backward(const ctn_tblock_desc* d, const ctn_tblock_params* p, con
     gb.A = L.G2; gb.W = w1t; gb.Wf = w1tf; gb.R = gy; gb.C = gx;
     gb.aop.stats = st1; gb.aop.alpha = p->alpha1; gb.aop.aux = sv->h1; gb.aop.apart = L.alphaSlab;
     gb.aop.aout = L.G1;
-    if (fold) gb.aop.fold = StatFold{L.slabD, L.partsD, cnt, 0.f, 1, nullptr};
-    else gb.aop.sums = L.sums1;
+    if (fold && (ws_fold_mask() & 2)) {
+      gb.aop.fold = StatFold{L.slabD, L.partsD, cnt, 0.f, 1, nullptr};
+    } else {
+      if (fold) CTN_HIP(launch_stats_finalize(L.slabD, G, L.partsD, cnt, 1, 0.f, L.sums1, s));
+      gb.aop.sums = L.sums1;
+    }
     CTN_HIP(launch_gemm_rows(dt, gb, s));
     nalpha = gemm_ws_grid(gb);
     // everything below only produces parameter gradients: fork to sw
