@@ -440,20 +440,21 @@ CTN_DEV float2 fold_stat(const StatFold& f, int m) {
   // Each lane sums its partials i = lane, lane+64, ... in that order; the loads of four
   // consecutive ones are issued together (a load-add chain would pay one memory latency
   // per partial, serially, at the start of every consumer workgroup).
+  // Every round issues its (up to) four loads before any add, the last, partial round
+  // too: as a serial load-add loop its one to three loads each paid a full memory
+  // latency in the prologue of every weight-stationary GEMM (same summation order).
   if (f.ws.grid == 0) {
     const double2* sg = f.slab + (size_t)m * f.parts;
-    int i = lane;
-    for (; i + 192 < f.parts; i += 256) {
-      const double2 v0 = sg[i], v1 = sg[i + 64], v2 = sg[i + 128], v3 = sg[i + 192];
-      s += v0.x; ss += v0.y;
-      s += v1.x; ss += v1.y;
-      s += v2.x; ss += v2.y;
-      s += v3.x; ss += v3.y;
-    }
-    for (; i < f.parts; i += 64) {
-      const double2 v = sg[i];
-      s += v.x;
-      ss += v.y;
+    for (int i = lane; i < f.parts; i += 256) {
+      double2 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = i + 64 * u < f.parts ? sg[i + 64 * u] : make_double2(0.0, 0.0);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (i + 64 * u < f.parts) {
+          s += v[u].x;
+          ss += v[u].y;
+        }
     }
   } else {
     const WsRuns& w = f.ws;
@@ -465,18 +466,16 @@ CTN_DEV float2 fold_stat(const StatFold& f, int m) {
       return t0 < ws_t0(w, b + 1) ? f.slab[((size_t)b * w.waves + wv) * w.kmax + (m - t0 / w.tpu)]
                                   : make_double2(0.0, 0.0);
     };
-    int i = lane;
-    for (; i + 192 < n; i += 256) {
-      const double2 v0 = get(i), v1 = get(i + 64), v2 = get(i + 128), v3 = get(i + 192);
-      s += v0.x; ss += v0.y;
-      s += v1.x; ss += v1.y;
-      s += v2.x; ss += v2.y;
-      s += v3.x; ss += v3.y;
-    }
-    for (; i < n; i += 64) {
-      const double2 v = get(i);
-      s += v.x;
-      ss += v.y;
+    for (int i = lane; i < n; i += 256) {
+      double2 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = i + 64 * u < n ? get(i + 64 * u) : make_double2(0.0, 0.0);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (i + 64 * u < n) {
+          s += v[u].x;
+          ss += v[u].y;
+        }
     }
   }
   s = wave_sum(s);
