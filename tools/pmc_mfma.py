@@ -12,7 +12,7 @@ json_out = sys.argv[2] if len(sys.argv) > 2 else None
 KINDS = {   # bench.py timer kinds -> kernel name (bf16 throughput mode)
     "1": "gemm_ws_kernel<0, 0, 1, 2, 8, 16, 2, 1>",
     "2": "dw_fwd_kernel<unsigned short, 0, 3, false>",
-    "3": "(anonymous namespace)::gemm_dual_ws_kernel<0, 6, 5, false>",   # the wave-specialised pair-A dual
+    "3": "gemm_dual_ws_kernel<0, 6, 5, false>",   # the wave-specialised pair-A dual
 }
 vals = defaultdict(lambda: defaultdict(list))
 for f in sorted(glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)):
@@ -20,7 +20,7 @@ for f in sorted(glob.glob(os.path.join(root, "**", "*counter_collection.csv"), r
         k = r["Kernel_Name"]
         if "ctn::" not in k:
             continue
-        k = k.split("(")[0].replace("void ctn::", "").replace("ctn::", "")
+        k = k.replace("(anonymous namespace)::", "").split("(")[0].replace("void ctn::", "").replace("ctn::", "")
         vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 def m(d, c):
     v = d.get(c)
