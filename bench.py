@@ -263,6 +263,13 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_ddp = world > 1 or args.ddp
     if use_ddp:
+        if "RANK" not in os.environ:      # --ddp without a launcher: a world of one rank
+            import socket
+            with socket.socket() as so:
+                so.bind(("127.0.0.1", 0))
+                port = so.getsockname()[1]
+            os.environ.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
+                              MASTER_PORT=str(port))
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         world = dist.get_world_size()    # what RCCL reports
