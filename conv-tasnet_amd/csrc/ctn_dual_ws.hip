@@ -61,7 +61,14 @@ constexpr bool DV_RB = CTN_DV_RAWB;
 #ifndef CTN_DV_NSL
 #define CTN_DV_NSL (CTN_DV_RAWB ? 6 : 4)
 #endif
-constexpr int DV_NSL = CTN_DV_NSL;               // LDS ring slots (NSL - 1 tiles in flight)
+constexpr int DV_NSL = CTN_DV_NSL;               // LDS ring slots
+// tiles a memory wave keeps in flight ahead of the one being consumed (<= NSL - 1: the
+// slot refilled is the one the consumers released last)
+#ifndef CTN_DV_PF
+#define CTN_DV_PF (CTN_DV_NSL - 1)
+#endif
+constexpr int DV_PF = CTN_DV_PF;
+static_assert(DV_PF >= 1 && DV_PF <= DV_NSL - 1, "ring look-ahead");
 // Column-wave split of the 256 x 128 dW2 slice: each of the 8 waves owns CJ 16-column
 // blocks x (16 / CJ) 16-row blocks (64 accumulator registers either way).  Fewer column
 // blocks per wave means fewer waves share (and, RAWB=1, transform) each B fragment, at
@@ -712,7 +719,7 @@ hipError_t launch_gemm_cols_ws(const GemmCols& c, hipStream_t s) {
   p.Bm = c.A; p.ldb = c.lda;    // the 128-channel slice: raw B
   p.Dpart = c.Cpart;            // [range][P][Q]
   const dim3 grid(gemm_cols_ws_ranges(c) * (c.P / DV_NS));
-  hipLaunchKernelGGL((gemm_dual_ws_kernel<NORM_GLN, DV_NSL, DV_NSL - 1, true>), grid, dim3((DV_NC + DV_NMW) * 64), 0,
+  hipLaunchKernelGGL((gemm_dual_ws_kernel<NORM_GLN, DV_NSL, DV_PF, true>), grid, dim3((DV_NC + DV_NMW) * 64), 0,
                      s, p);
   return hipGetLastError();
 }
@@ -721,9 +728,9 @@ hipError_t launch_gemm_dual_ws(const GemmDual& p, hipStream_t s) {
   if (!gemm_dual_ws_eligible(p)) return hipErrorInvalidValue;
   const dim3 grid(gemm_dual_ws_ranges(p) * (p.Nout / DV_NS));
   if (p.norm == NORM_GLN)
-    hipLaunchKernelGGL((gemm_dual_ws_kernel<NORM_GLN, DV_NSL, DV_NSL - 1>), grid, dim3(DV_NT), 0, s, p);
+    hipLaunchKernelGGL((gemm_dual_ws_kernel<NORM_GLN, DV_NSL, DV_PF>), grid, dim3(DV_NT), 0, s, p);
   else
-    hipLaunchKernelGGL((gemm_dual_ws_kernel<NORM_CLN, DV_NSL, DV_NSL - 1>), grid, dim3(DV_NT), 0, s, p);
+    hipLaunchKernelGGL((gemm_dual_ws_kernel<NORM_CLN, DV_NSL, DV_PF>), grid, dim3(DV_NT), 0, s, p);
   return hipGetLastError();
 }
 
