@@ -6,7 +6,9 @@ One step = forward + PIT SI-SNR loss + backward + clip_grad_norm_(5) + Adam
 mixtures already resident in HBM.  Workload: paper config (N=256 L=20 B=256
 H=512 P=3 X=8 R=4 gLN, 2 speakers, 4 s @ 8 kHz), 32 utterances per GPU, bf16
 activations (fp32 params/stats/accumulation).  N GPUs = one process per GPU
-under torchrun, DDP over RCCL (weak scaling: per-GPU batch fixed).
+under torchrun, the gradients averaged over RCCL with one flat all-reduce after
+backward (ctn_dist.FlatGradAllReduce; CTN_GRAD_SYNC=ddp for DistributedDataParallel)
+(weak scaling: per-GPU batch fixed).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
@@ -246,7 +248,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--timer-kind", type=int, default=TIMER_GEMM_BWD_A)
     ap.add_argument("--ddp", action="store_true",
-                    help="DDP over RCCL even at world size 1 (exercises process-group init, bucket hooks)")
+                    help="the data-parallel path over RCCL even at world size 1 (process-group init, "
+                         "gradient exchange)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -299,7 +302,17 @@ def main():
     # parameter-gradient reductions of all blocks batched at the end of backward (on by
     # default; CTN_DEFER_REDUCE=0 for A/B against the per-block reductions)
     model.defer_grad_reduce = os.environ.get("CTN_DEFER_REDUCE", "1") == "1"
-    if use_ddp:
+    # gradient exchange across ranks: "flat" (default) = one all-reduce of all gradients
+    # after backward (ctn_dist.FlatGradAllReduce; the deferred reductions stay on),
+    # "ddp" = DistributedDataParallel's bucket hooks during backward (per-block reductions)
+    sync_kind = os.environ.get("CTN_GRAD_SYNC", "flat")
+    if sync_kind not in ("flat", "ddp"):
+        sys.exit(f"bench.py: CTN_GRAD_SYNC={sync_kind} (flat|ddp)")
+    grad_sync = None
+    if use_ddp and sync_kind == "flat":
+        import ctn_dist
+        grad_sync = ctn_dist.FlatGradAllReduce(model.parameters())
+    elif use_ddp:
         # gradients as views into the RCCL buckets (no per-step copy into the buckets),
         # one fixed graph (the reducer skips its unused-parameter search each step)
         model = torch.nn.parallel.DistributedDataParallel(
@@ -318,6 +331,8 @@ def main():
         loss = pc.cal_loss(src, est, lens)[0]
         opt.zero_grad(set_to_none=True)
         loss.backward()
+        if grad_sync is not None:
+            grad_sync.sync()
         ctn_optim.clip_grad_norm_(model.parameters(), 5.0)
         opt.step()
         return loss
@@ -396,7 +411,8 @@ def main():
                                     f"{'causal' if cfg['causal'] else 'non-causal'} relu-mask, {C} spk, "
                                     f"{args.seconds:g} s @ {rate // 1000} kHz, fwd+PIT loss+bwd+clip+Adam"),
                        "per_gpu_batch": M, "global_batch": M * world, "samples": T, "frames": K,
-                       "parallelism": f"dp{world}" + (" (DDP/RCCL)" if use_ddp else ""),
+                       "parallelism": f"dp{world}" + ((" (DDP/RCCL)" if grad_sync is None else
+                                                                     " (flat all-reduce/RCCL)") if use_ddp else ""),
                        "rccl_world_size": dist.get_world_size() if use_ddp else None,
                        "rank_ms_per_step": rank_ms,
                        # TemporalBlock backwards per step whose parameter-gradient reductions

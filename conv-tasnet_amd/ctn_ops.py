@@ -194,6 +194,20 @@ def _pending_uses(p) -> int:
 
 DEFERRED_BLOCKS = 0   # block backwards that took the deferred path (tests, bench)
 
+# parameters whose gradients a post-backward exchange (ctn_dist.FlatGradAllReduce)
+# consumes: id -> weak reference; under torch.distributed only these may be written late
+_SYNCED = {}
+
+
+def register_synced_after_backward(params):
+    for p in params:
+        _SYNCED[id(p)] = weakref.ref(p)
+
+
+def _synced_after_backward(p) -> bool:
+    r = _SYNCED.get(id(p))
+    return r is not None and r() is p
+
 
 class _TaskState:
     """What one backward pass (device, autograd graph task) leaves for its end: the
@@ -247,12 +261,14 @@ def _grads_unobserved(ctx) -> bool:
     nothing can observe the gradients before the backward pass ends: a plain
     .backward() that will accumulate into every one of these leaves (not
     autograd.grad), no gradient yet (no accumulation), no hooks, fp32 contiguous
-    leaves, no torch.distributed (DDP hooks read gradients as they arrive)."""
+    leaves; under torch.distributed only parameters a post-backward exchange consumes
+    (ctn_dist.FlatGradAllReduce: DDP's hooks read gradients as they arrive)."""
     if torch.is_grad_enabled() or not hasattr(ctx, "param_refs"):
         return False
-    if torch.distributed.is_available() and torch.distributed.is_initialized():
-        return False
+    dist_on = torch.distributed.is_available() and torch.distributed.is_initialized()
     for p, node in zip(ctx.param_refs, ctx.acc_nodes):
+        if dist_on and not _synced_after_backward(p):
+            return False
         if _pending_uses(p) != 1:    # another pending use of this parameter
             return False
         if (node is None or p.grad is not None or p.dtype != torch.float32 or not p.is_contiguous()

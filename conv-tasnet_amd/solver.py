@@ -216,6 +216,8 @@ class Solver(object):
                 loss = cal_loss(source, self.model(mixture), lengths)[0]
                 self.optimizer.zero_grad()
                 loss.backward()
+                if getattr(self.model, "grad_sync", None) is not None:   # train.FlatDP
+                    self.model.grad_sync.sync()
                 clip(self.model.parameters(), self.max_norm)
                 self.optimizer.step()
             running += loss.detach().double()

@@ -127,6 +127,18 @@ class Single(torch.nn.Module):
         return self.module(*args, **kwargs)
 
 
+class FlatDP(Single):
+    """One process per GPU: the gradients are averaged across ranks by one flat RCCL
+    all-reduce after backward (ctn_dist.FlatGradAllReduce, run by the solver), which keeps
+    the TemporalBlock gradient reductions deferred and batched; DistributedDataParallel's
+    hooks need every gradient as it arrives (bench: 2110 vs 1990 utt/s at world size 1)."""
+
+    def __init__(self, module):
+        super().__init__(module)
+        import ctn_dist
+        self.grad_sync = ctn_dist.FlatGradAllReduce(module.parameters())
+
+
 def main(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -156,11 +168,16 @@ def main(args):
         print(model)
     if args.use_cuda:
         model.cuda()
-        # gradients as views into the RCCL buckets and a static graph: at world size 1
-        # on one MI355X this took the DDP step from 21.8 to 18.8 ms (plain 18.3 ms)
-        model = (torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], gradient_as_bucket_view=True,
-                                                           static_graph=True)
-                 if world > 1 else Single(model))
+        if world == 1:
+            model = Single(model)
+        elif args.norm_type != 'BN':
+            model = FlatDP(model)
+        else:
+            # BatchNorm: DDP also broadcasts rank 0's running statistics each forward.
+            # Gradients as views into the RCCL buckets and a static graph: at world size 1
+            # on one MI355X this took the DDP step from 21.8 to 18.8 ms (plain 18.3 ms)
+            model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], gradient_as_bucket_view=True,
+                                                              static_graph=True)
     else:
         model = Single(model)
     # optimizer

@@ -1,7 +1,9 @@
 """Multi-process data parallelism on CPU (gloo, world_size 2): the DDP gradient
 all-reduce over equal per-rank shards reproduces the single-process full-batch
 gradient of the reference loss (loss = -mean over the batch,
-DDP averages rank gradients), and the bench's max-over-ranks timing reduction.
+DDP averages rank gradients), the bench's flat post-backward exchange
+(ctn_dist.FlatGradAllReduce) gives DDP's gradients to the bit, and the bench's
+max-over-ranks timing reduction.
 The model here is the CPU oracle wrapped in an nn.Module — the HIP path runs the
 same DDP wrapper on RCCL on the GPU box."""
 import os
@@ -38,6 +40,7 @@ def _free_port():
 def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    import train
     torch.manual_seed(0)
     params = O.init_params(CFG, 7)
     mix, src = O.synth_batch(4, CFG.C, 400, 3)
@@ -48,9 +51,20 @@ def _worker(rank, world, port, q):
     loss = O.cal_loss(src[shard], est, lens[shard])[0]
     loss.backward()
     grads = [p.grad.clone() for p in model.module.p]
+    # the bench's / train.py's exchange: one flat all-reduce after backward.  Rank 1 starts
+    # from perturbed weights, which the constructor's broadcast from rank 0 replaces.
+    plain = OracleModel(params)
+    if rank == 1:
+        with torch.no_grad():
+            for p in plain.p:
+                p.add_(1.0)
+    net = train.FlatDP(plain)                # train.py's wrapper for world size > 1
+    O.cal_loss(src[shard], net(mix[shard]), lens[shard])[0].backward()
+    net.grad_sync.sync()                     # what solver.py runs after backward
+    flat = [p.grad.clone() for p in plain.p]
     t = torch.tensor([0.1 * (rank + 1)], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)                  # bench.py timing reduction
-    q.put((rank, [g.numpy() for g in grads], float(t)))
+    q.put((rank, [g.numpy() for g in grads], float(t), [g.numpy() for g in flat]))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -72,10 +86,12 @@ def test_ddp_two_ranks_match_full_batch():
     params = O.init_params(CFG, 7)
     mix, src = O.synth_batch(4, CFG.C, 400, 3)
     _, _, _, grads = O.fwd_bwd(CFG, params, mix, src, torch.tensor([400] * 4))
-    for (_, g_rank, tmax) in res:
+    for (_, g_rank, tmax, g_flat) in res:
         assert abs(tmax - 0.2) < 1e-12
         for n, gr in zip([n for n, _ in O.param_shapes(CFG)], g_rank):
             torch.testing.assert_close(torch.from_numpy(gr), grads[n], rtol=1e-4, atol=1e-6)
+        for a, b in zip(g_rank, g_flat):     # the flat exchange averages exactly as DDP does
+            assert (a == b).all()
     # both ranks hold identical gradients after the all-reduce
     for a, b in zip(res[0][1], res[1][1]):
         assert (a == b).all()

@@ -9,7 +9,9 @@ on the reduced gradients (train.py / bench.py's step, replacing
 src/train.py:120-122's DataParallel).  Checked against the single-process
 full-batch HIP step: averaged gradients equal the full-batch gradients (loss =
 batch mean, equal shards), and both ranks end with identical parameters.
-fp32 (tight) and bf16 with packed weights (the throughput mode).  GPU only.
+fp32 (tight) and bf16 with packed weights (the throughput mode).  The same with the
+bench's default exchange, ctn_dist.FlatGradAllReduce (one all-reduce after backward,
+the TemporalBlock gradient reductions deferred to the end of the pass).  GPU only.
 """
 import os
 import socket
@@ -38,8 +40,9 @@ def _batch():
     return synthetic.speech_like(M, CFG["C"], T, 21)
 
 
-def _step(model, mix, src, bf16):
-    """forward -> cal_loss -> zero_grad -> backward -> clip(5) -> Adam (solver.py:178-186)."""
+def _step(model, mix, src, bf16, sync=None):
+    """forward -> cal_loss -> zero_grad -> backward [-> flat gradient all-reduce] ->
+    clip(5) -> Adam (solver.py:178-186)."""
     import ctn_optim
     import pit_criterion as pc
     opt = ctn_optim.Adam(model.parameters(), lr=1e-3)
@@ -50,6 +53,8 @@ def _step(model, mix, src, bf16):
     loss = pc.cal_loss(src, est, lens)[0]
     opt.zero_grad()
     loss.backward()
+    if sync is not None:
+        sync.sync()
     grads = [p.grad.detach().cpu().clone() for p in model.parameters()]
     ctn_optim.clip_grad_norm_(model.parameters(), 5.0)
     opt.step()
@@ -63,15 +68,26 @@ def _worker(rank, world, port, bf16, view, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import conv_tasnet as ct
+        import ctn_dist
+        import ctn_ops
         dev = torch.device("cuda", 0)
         torch.manual_seed(0)
         model = ct.ConvTasNet(**CFG).to(dev)
-        # view: the bench / train.py options (gradients as bucket views, static graph)
-        ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[0], bucket_cap_mb=0.1,
-                                                        gradient_as_bucket_view=view, static_graph=view)
+        sync = None
+        if view == "flat":
+            # the bench's default: one flat all-reduce after backward, deferred reductions on
+            sync = ctn_dist.FlatGradAllReduce(model.parameters())
+            net = model
+        else:
+            # view: the bench / train.py options (gradients as bucket views, static graph)
+            net = torch.nn.parallel.DistributedDataParallel(model, device_ids=[0], bucket_cap_mb=0.1,
+                                                            gradient_as_bucket_view=view, static_graph=view)
         mix, src = _batch()
         shard = slice(rank * (M // world), (rank + 1) * (M // world))
-        loss, grads, params = _step(ddp, mix[shard].to(dev), src[shard].to(dev), bf16)
+        n0 = ctn_ops.DEFERRED_BLOCKS
+        loss, grads, params = _step(net, mix[shard].to(dev), src[shard].to(dev), bf16, sync)
+        # deferral under torch.distributed only for the post-backward exchange
+        assert (ctn_ops.DEFERRED_BLOCKS > n0) == (view == "flat"), ctn_ops.DEFERRED_BLOCKS - n0
         q.put((rank, loss, [g.numpy() for g in grads], [p.numpy() for p in params]))
         dist.barrier()
     finally:
@@ -79,7 +95,8 @@ def _worker(rank, world, port, bf16, view, q):
 
 
 @pytest.mark.timeout(400)
-@pytest.mark.parametrize("bf16,view", [(False, False), (True, False), (False, True)])
+@pytest.mark.parametrize("bf16,view", [(False, False), (True, False), (False, True), (False, "flat"),
+                                       (True, "flat")])
 def test_ddp_two_ranks_hip_model_matches_full_batch(bf16, view):
     import conv_tasnet as ct
     ctx = mp.get_context("spawn")
