@@ -61,13 +61,16 @@ class FlatGradAllReduce:
     def sync(self):
         """All-reduce (mean) every parameter gradient; a parameter without a gradient on
         this rank contributes zeros (DDP's treatment of an unused parameter) and receives
-        the mean."""
+        the mean.  Afterwards each ``p.grad`` is a new tensor, a view into the reduced
+        buffer (as DDP's gradient_as_bucket_view makes them), not the one backward wrote."""
         for p in self.params:
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
-        for bucket in self._buckets([p.grad for p in self.params]):
-            flat = _flatten_dense_tensors(bucket)      # one concatenation launch
+        for bucket in self._buckets(self.params):
+            flat = _flatten_dense_tensors([p.grad for p in bucket])   # one concatenation launch
             flat.div_(self.world)
             dist.all_reduce(flat, group=self.group)
-            # one multi-tensor launch back (a copy_ per gradient was ≈300 launches, 0.7 ms)
-            torch._foreach_copy_(bucket, _unflatten_dense_tensors(flat, bucket))
+            # the averaged gradients become views into the reduced buffer: no copy back (a
+            # copy_ per gradient was ≈300 launches, 0.7 ms; one multi-tensor copy 0.15 ms)
+            for p, v in zip(bucket, _unflatten_dense_tensors(flat, bucket)):
+                p.grad = v
