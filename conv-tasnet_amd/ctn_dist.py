@@ -11,8 +11,8 @@ write its parameter gradients immediately (68 reduction launches per step at the
 shape) instead of the one batched reduction at the end of the pass
 (ConvTasNet.defer_grad_reduce, ctn_ops._end_of_backward).  ``FlatGradAllReduce``
 consumes the gradients only after ``backward()`` returns, so the deferred reductions
-stay on, and exchanges them as ONE flat buffer per dtype: one ring all-reduce of the
-whole model (≈35 MB fp32 for the paper configuration) — a single large message is what
+stay on and write straight into its persistent gradient buffer, and exchanges that
+buffer with ONE all-reduce per dtype: one ring all-reduce of the whole model (≈35 MB fp32 for the paper configuration) — a single large message is what
 point-to-point xGMI rings move at full link rate.
 
 Averaging matches DDP's: every gradient is divided by the world size, then summed
@@ -48,7 +48,17 @@ class FlatGradAllReduce:
                                group=group)
                 for p, v in zip(bucket, _unflatten_dense_tensors(flat, bucket)):
                     p.copy_(v)
-        ctn_ops.register_synced_after_backward(self.params)
+        # one persistent gradient buffer per (device, dtype); each parameter owns a view.
+        # The deferred TemporalBlock backwards write their gradients straight into it, so
+        # after a backward pass most gradients are already in place.
+        self._arenas = []
+        views = {}
+        for bucket in self._buckets(self.params):
+            flat = torch.empty(sum(p.numel() for p in bucket), device=bucket[0].device, dtype=bucket[0].dtype)
+            vs = _unflatten_dense_tensors(flat, bucket)
+            self._arenas.append((bucket, flat, vs))
+            views.update({id(p): v for p, v in zip(bucket, vs)})
+        ctn_ops.register_synced_after_backward(self.params, [views[id(p)] for p in self.params])
 
     @staticmethod
     def _buckets(tensors):
@@ -61,16 +71,18 @@ class FlatGradAllReduce:
     def sync(self):
         """All-reduce (mean) every parameter gradient; a parameter without a gradient on
         this rank contributes zeros (DDP's treatment of an unused parameter) and receives
-        the mean.  Afterwards each ``p.grad`` is a new tensor, a view into the reduced
-        buffer (as DDP's gradient_as_bucket_view makes them), not the one backward wrote."""
-        for p in self.params:
-            if p.grad is None:
-                p.grad = torch.zeros_like(p)
-        for bucket in self._buckets(self.params):
-            flat = _flatten_dense_tensors([p.grad for p in bucket])   # one concatenation launch
+        the mean.  Afterwards each ``p.grad`` is the parameter's view of the persistent
+        buffer (as DDP's gradient_as_bucket_view makes them): keep a copy, not the tensor,
+        to hold a gradient past the next step."""
+        for bucket, flat, views in self._arenas:
+            for p, v in zip(bucket, views):
+                g = p.grad
+                if g is v:               # written in place by a deferred block backward
+                    continue
+                if g is None:
+                    v.zero_()
+                else:                    # accumulated elsewhere (encoder, decoder, ...)
+                    v.copy_(g)
+                p.grad = v
             flat.div_(self.world)
             dist.all_reduce(flat, group=self.group)
-            # the averaged gradients become views into the reduced buffer: no copy back (a
-            # copy_ per gradient was ≈300 launches, 0.7 ms; one multi-tensor copy 0.15 ms)
-            for p, v in zip(bucket, _unflatten_dense_tensors(flat, bucket)):
-                p.grad = v

@@ -195,18 +195,28 @@ def _pending_uses(p) -> int:
 DEFERRED_BLOCKS = 0   # block backwards that took the deferred path (tests, bench)
 
 # parameters whose gradients a post-backward exchange (ctn_dist.FlatGradAllReduce)
-# consumes: id -> weak reference; under torch.distributed only these may be written late
+# consumes: id -> (weak reference, the exchange's persistent gradient view or None); under
+# torch.distributed only these may be written late, and a deferred block backward writes
+# their gradients straight into the exchange's buffer
 _SYNCED = {}
 
 
-def register_synced_after_backward(params):
-    for p in params:
-        _SYNCED[id(p)] = weakref.ref(p)
+def register_synced_after_backward(params, grad_views=None):
+    for i, p in enumerate(params):
+        _SYNCED[id(p)] = (weakref.ref(p), None if grad_views is None else grad_views[i])
 
 
 def _synced_after_backward(p) -> bool:
-    r = _SYNCED.get(id(p))
-    return r is not None and r() is p
+    e = _SYNCED.get(id(p))
+    return e is not None and e[0]() is p
+
+
+def _grad_buffer(p):
+    """A new gradient for parameter p: its view of the exchange buffer, or fresh memory."""
+    e = _SYNCED.get(id(p))
+    if e is not None and e[1] is not None and e[0]() is p:
+        return e[1]
+    return torch.empty_like(p)
 
 
 class _TaskState:
@@ -344,13 +354,15 @@ class TBlockFn(torch.autograd.Function):
                                  *ctx.bn, *(ctx.pack[4:8] if ctx.pack else (None,) * 4))
         saved = L.TBlockSaved(h1.data_ptr(), d.data_ptr(), stats.data_ptr())
         gx = torch.empty_like(x)
-        grads = [torch.empty_like(p) for p in params]
-        gstruct = L.TBlockGrads(*[g.data_ptr() for g in grads])
         late_ok = (ctx.defer or ctx.wgrad_split) and _grads_unobserved(ctx)
         if getattr(ctx, "use_token", None) is not None:
             _task_state(x.device).tokens.append(weakref.ref(ctx.use_token))   # spent at the pass's end
         if ctx.defer and not ctx.wgrad_split and late_ok:
+            grads = [_grad_buffer(p) for p in ctx.param_refs]
+            gstruct = L.TBlockGrads(*[g.data_ptr() for g in grads])
             return TBlockFn._backward_deferred(ctx, lib, desc, pstruct, saved, x, gy, gx, grads, gstruct)
+        grads = [torch.empty_like(p) for p in params]
+        gstruct = L.TBlockGrads(*[g.data_ptr() for g in grads])
         nb = lib.ctn_tblock_workspace_bytes(ctypes.byref(desc), 1)
         ws = L.workspace(nb, x.device)
         if not (ctx.wgrad_split and late_ok):

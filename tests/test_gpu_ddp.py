@@ -84,6 +84,15 @@ def _worker(rank, world, port, bf16, view, q):
                                                             gradient_as_bucket_view=view, static_graph=view)
         mix, src = _batch()
         shard = slice(rank * (M // world), (rank + 1) * (M // world))
+        if sync is not None:
+            # one exchange before the measured step: the step's deferred blocks then write
+            # into a persistent gradient buffer that already holds gradients
+            import pit_criterion as pc
+            model.act_dtype = torch.bfloat16 if bf16 else torch.float32
+            lens = torch.full((M // world,), T, dtype=torch.int64, device=dev)
+            pc.cal_loss(src[shard].to(dev), net(mix[shard].to(dev)), lens)[0].backward()
+            sync.sync()
+            model.zero_grad(set_to_none=True)
         n0 = ctn_ops.DEFERRED_BLOCKS
         loss, grads, params = _step(net, mix[shard].to(dev), src[shard].to(dev), bf16, sync)
         # deferral under torch.distributed only for the post-backward exchange

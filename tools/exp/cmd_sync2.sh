@@ -1,10 +1,10 @@
-# round 4: flat exchange with gradients as views of the reduced buffer; A/B against the plain step + trace
+# round 4: flat exchange over a persistent gradient buffer the deferred blocks write into; A/B against the plain step + trace
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-T=${1:-r4sync3}
+T=${1:-r4sync4}
 O=gpurun_out/$T; mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest -x -v --timeout 400 --timeout-method thread tests/test_gpu_ddp.py -k flat > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+timeout -k 10 600 python -u -m pytest -x -v --timeout 400 --timeout-method thread tests/test_gpu_ddp.py tests/test_gpu_defer_reduce.py > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
 for i in 1 2; do
   timeout -k 10 300 python bench.py --no-cpu-baseline > $O/plain$i.json 2> $O/plain$i.err || exit 1
