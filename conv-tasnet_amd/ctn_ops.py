@@ -203,7 +203,8 @@ _SYNCED = {}
 
 def register_synced_after_backward(params, grad_views=None):
     for i, p in enumerate(params):
-        _SYNCED[id(p)] = (weakref.ref(p), None if grad_views is None else grad_views[i])
+        # the view by weak reference: the exchange object owns its buffer
+        _SYNCED[id(p)] = (weakref.ref(p), None if grad_views is None else weakref.ref(grad_views[i]))
 
 
 def _synced_after_backward(p) -> bool:
@@ -215,7 +216,9 @@ def _grad_buffer(p):
     """A new gradient for parameter p: its view of the exchange buffer, or fresh memory."""
     e = _SYNCED.get(id(p))
     if e is not None and e[1] is not None and e[0]() is p:
-        return e[1]
+        v = e[1]()
+        if v is not None:
+            return v
     return torch.empty_like(p)
 
 

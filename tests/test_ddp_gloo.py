@@ -95,3 +95,21 @@ def test_ddp_two_ranks_match_full_batch():
     # both ranks hold identical gradients after the all-reduce
     for a, b in zip(res[0][1], res[1][1]):
         assert (a == b).all()
+
+
+def test_grad_buffer_registry():
+    """ctn_ops hands a deferred block backward the exchange's view of a parameter's
+    gradient while the exchange (its owner) lives, fresh memory after."""
+    import ctn_ops
+    p = torch.nn.Parameter(torch.zeros(3, 4))
+    q = torch.nn.Parameter(torch.zeros(5))
+    buf = torch.empty(12)
+    v = buf.view(3, 4)
+    assert not ctn_ops._synced_after_backward(p)
+    ctn_ops.register_synced_after_backward([p], [v])
+    assert ctn_ops._synced_after_backward(p) and not ctn_ops._synced_after_backward(q)
+    assert ctn_ops._grad_buffer(p) is v
+    assert ctn_ops._grad_buffer(q).shape == (5,)
+    del v, buf
+    g = ctn_ops._grad_buffer(p)
+    assert g.shape == (3, 4) and ctn_ops._synced_after_backward(p)

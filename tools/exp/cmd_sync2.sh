@@ -1,7 +1,7 @@
 # round 4: flat exchange over a persistent gradient buffer the deferred blocks write into; A/B against the plain step + trace
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-T=${1:-r4sync4}
+T=${1:-r4sync5}
 O=gpurun_out/$T; mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest -x -v --timeout 400 --timeout-method thread tests/test_gpu_ddp.py tests/test_gpu_defer_reduce.py > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
