@@ -366,7 +366,7 @@ def main():
         dist.all_gather(ts, t)
         rank_ms = [round(float(x) / args.steps * 1e3, 3) for x in ts]
         elapsed = max(float(x) for x in ts)
-    final_loss = float(loss)
+    final_loss = float(loss.detach())
     deferred = (ctn_ops.DEFERRED_BLOCKS - n_def0) / args.steps
 
     if rank == 0:
