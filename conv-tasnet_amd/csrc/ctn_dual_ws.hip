@@ -69,6 +69,12 @@ constexpr int DV_NSL = CTN_DV_NSL;               // LDS ring slots
 #endif
 constexpr int DV_PF = CTN_DV_PF;
 static_assert(DV_PF >= 1 && DV_PF <= DV_NSL - 1, "ring look-ahead");
+// the cLN form (c4's causal blocks) may take its own look-ahead
+#ifndef CTN_DV_PF_CLN
+#define CTN_DV_PF_CLN CTN_DV_PF
+#endif
+constexpr int DV_PF_CLN = CTN_DV_PF_CLN;
+static_assert(DV_PF_CLN >= 1 && DV_PF_CLN <= DV_NSL - 1, "ring look-ahead (cLN)");
 // Column-wave split of the 256 x 128 dW2 slice: each of the 8 waves owns CJ 16-column
 // blocks x (16 / CJ) 16-row blocks (64 accumulator registers either way).  Fewer column
 // blocks per wave means fewer waves share (and, RAWB=1, transform) each B fragment, at
@@ -730,7 +736,7 @@ hipError_t launch_gemm_dual_ws(const GemmDual& p, hipStream_t s) {
   if (p.norm == NORM_GLN)
     hipLaunchKernelGGL((gemm_dual_ws_kernel<NORM_GLN, DV_NSL, DV_PF>), grid, dim3(DV_NT), 0, s, p);
   else
-    hipLaunchKernelGGL((gemm_dual_ws_kernel<NORM_CLN, DV_NSL, DV_PF>), grid, dim3(DV_NT), 0, s, p);
+    hipLaunchKernelGGL((gemm_dual_ws_kernel<NORM_CLN, DV_NSL, DV_PF_CLN>), grid, dim3(DV_NT), 0, s, p);
   return hipGetLastError();
 }
 
