@@ -212,6 +212,13 @@ def spawn_ranks(n, cmd, port=None, env=None):
     return rc
 
 
+def _rehearsal() -> bool:
+    """CTN_BENCH_REHEARSAL=1: the N-rank job on ONE GPU over gloo, to exercise the
+    multi-rank code path (launcher, exchange, timing reduction) on a one-GPU box; its
+    numbers are not a measurement."""
+    return os.environ.get("CTN_BENCH_REHEARSAL", "0") == "1"
+
+
 def visible_gpus():
     """GPUs this process may use, without initialising HIP in this process: the
     *_VISIBLE_DEVICES lists if set, else the GPU nodes of the KFD topology (sysfs)."""
@@ -256,7 +263,7 @@ def main():
         # no outside launcher: start one rank per GPU ourselves (children, no exec); the
         # GPUs are counted from the environment / sysfs, so this parent never loads HIP
         visible = visible_gpus()
-        if args.gpus > visible:
+        if args.gpus > visible and not _rehearsal():
             sys.exit(f"bench.py: --gpus {args.gpus} but only {visible} GPU(s) visible")
         sys.exit(spawn_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -264,6 +271,8 @@ def main():
         sys.exit(f"bench.py: --gpus {args.gpus} disagrees with WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if _rehearsal():
+        local = 0     # every rank on the one GPU (gloo: RCCL refuses two ranks per device)
     use_ddp = world > 1 or args.ddp
     if use_ddp:
         if "RANK" not in os.environ:      # --ddp without a launcher: a world of one rank
@@ -274,7 +283,10 @@ def main():
             os.environ.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
                               MASTER_PORT=str(port))
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if _rehearsal():
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         world = dist.get_world_size()    # what RCCL reports
     dev = torch.device("cuda", local)
 
@@ -412,7 +424,8 @@ def main():
                                     f"{args.seconds:g} s @ {rate // 1000} kHz, fwd+PIT loss+bwd+clip+Adam"),
                        "per_gpu_batch": M, "global_batch": M * world, "samples": T, "frames": K,
                        "parallelism": f"dp{world}" + ((" (DDP/RCCL)" if grad_sync is None else
-                                                                     " (flat all-reduce/RCCL)") if use_ddp else ""),
+                                                                     " (flat all-reduce/RCCL)") if use_ddp else "")
+                                      + (" REHEARSAL: all ranks on one GPU over gloo" if _rehearsal() else ""),
                        "rccl_world_size": dist.get_world_size() if use_ddp else None,
                        "rank_ms_per_step": rank_ms,
                        # TemporalBlock backwards per step whose parameter-gradient reductions
