@@ -426,7 +426,7 @@ def main():
                        "parallelism": f"dp{world}" + ((" (DDP/RCCL)" if grad_sync is None else
                                                                      " (flat all-reduce/RCCL)") if use_ddp else "")
                                       + (" REHEARSAL: all ranks on one GPU over gloo" if _rehearsal() else ""),
-                       "rccl_world_size": dist.get_world_size() if use_ddp else None,
+                       "rccl_world_size": dist.get_world_size() if use_ddp and not _rehearsal() else None,
                        "rank_ms_per_step": rank_ms,
                        # TemporalBlock backwards per step whose parameter-gradient reductions
                        # ran batched at the end of backward (ctn_tblock_reduce_grads)
