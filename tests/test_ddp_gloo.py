@@ -113,3 +113,40 @@ def test_grad_buffer_registry():
     del v, buf
     g = ctn_ops._grad_buffer(p)
     assert g.shape == (3, 4) and ctn_ops._synced_after_backward(p)
+
+
+def _flat_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import ctn_dist
+    a = torch.nn.Parameter(torch.full((4,), float(rank)))     # broadcast: rank 0's zeros win
+    b = torch.nn.Parameter(torch.zeros(2, 3))
+    sync = ctn_dist.FlatGradAllReduce([a, b])
+    for step in range(2):                                      # the buffer is reused
+        a.grad = torch.full((4,), float(rank + 1 + step))
+        b.grad = None if rank == 1 else torch.full((2, 3), 3.0 * rank)   # unused on rank 1
+        sync.sync()
+        q.put((rank, step, a.detach().clone(), a.grad.clone(), b.grad.clone()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_flat_exchange_mean_unused_and_reuse():
+    """World size 3: the exchange averages (a non-power-of-two world), an unused parameter
+    contributes zeros, the persistent buffer is reused across steps, and the constructor
+    broadcasts rank 0's weights."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_flat_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(6)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, step, a, ga, gb in res:
+        assert torch.equal(a, torch.zeros(4))
+        torch.testing.assert_close(ga, torch.full((4,), (1 + 2 + 3) / 3 + step))
+        torch.testing.assert_close(gb, torch.full((2, 3), (0.0 + 0.0 + 6.0) / 3))
