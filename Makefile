@@ -17,7 +17,19 @@ DEVFLAGS := -mllvm -amdgpu-mfma-vgpr-form -Xclang -target-feature -Xclang -packe
 CXXFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function -Iinclude $(DEVFLAGS)
 LIB      := $(PKG)/libctn_hip.so
 
-all: $(LIB)
+# Debug variant for tests/test_gpu_spin_timeout.py: every LDS generation-word wait gives up
+# after one poll (CTN_SPIN_LIMIT=1), so the wave-specialised kernels take their timeout path
+# and must report it through the device error word instead of hanging or passing silently.
+SPIN_LIB := $(PKG)/libctn_hip_spin1.so
+SPIN_OBJ := build/spin1/ctn_dual_ws.o build/spin1/ctn_gemm_ws.o
+all: $(LIB) $(SPIN_LIB)
+
+build/spin1/%.o: $(PKG)/csrc/%.hip $(HDR) Makefile
+	@mkdir -p build/spin1
+	$(HIPCC) $(CXXFLAGS) -DCTN_SPIN_LIMIT=1 -c $< -o $@
+
+$(SPIN_LIB): $(SPIN_OBJ) $(filter-out build/ctn_dual_ws.o build/ctn_gemm_ws.o,$(OBJ))
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^
 
 build/%.o: $(PKG)/csrc/%.hip $(HDR) Makefile
 	@mkdir -p build
@@ -27,7 +39,7 @@ $(LIB): $(OBJ)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJ)
 
 clean:
-	rm -rf build $(LIB)
+	rm -rf build $(LIB) $(SPIN_LIB)
 
 .PHONY: all clean
 

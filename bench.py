@@ -51,12 +51,22 @@ CONFIGS = {
     "c5": (dict(PAPER, N=512, C=3), 8000, 8.0, 16),
 }
 
-# timer kinds (include/ctn.h ctn_timer_enable)
-TIMER_GEMM1, TIMER_DW_FWD, TIMER_GEMM_BWD_A = 1, 2, 3
+# timer kinds (include/ctn.h CTN_TIMER_*): the TemporalBlock's seven kernel families
+TIMER_GEMM1, TIMER_DW_FWD, TIMER_GEMM_BWD_A, TIMER_DW_BWD, TIMER_GEMM_GX, TIMER_COLS_W1, TIMER_GEMM2 = range(1, 8)
+TIMER_NAMES = {
+    TIMER_GEMM1: "gemm_ws fwd 1x1 B->H (PReLU-stats epilogue)",
+    TIMER_DW_FWD: "dw_fwd (norm1 + depthwise + PReLU-2 stats)",
+    TIMER_GEMM_BWD_A: "gemm_dual bwd g_n2 = gy.W2 (norm-backward epilogue) + dW2 = gy^T.n2",
+    TIMER_DW_BWD: "dw_bwd (norm2/PReLU2 bwd + transposed depthwise + dW_dw + norm1 sums)",
+    TIMER_GEMM_GX: "gemm_ws bwd gx = n1bwd(g).W1 + gy (stores dL/dh1)",
+    TIMER_COLS_W1: "gemm_cols bwd dW1 = (dL/dh1)^T.x",
+    TIMER_GEMM2: "gemm_ws fwd 1x1 H->B (norm2 operand, residual)",
+}
 
 
 def kernel_bytes(kind, M, K, cfg, s=2):
-    """Algorithmic HBM bytes per launch of the timed kernel family."""
+    """Algorithmic HBM bytes per launch of the timed kernel family:
+    each operand row read once and each output row written once, weights once."""
     B, H = cfg["B"], cfg["H"]
     rows = M * K
     if kind == TIMER_GEMM1:        # x[B] in, h1[H] out, W1 once
@@ -65,7 +75,34 @@ def kernel_bytes(kind, M, K, cfg, s=2):
         return rows * 2 * H * s
     if kind == TIMER_GEMM_BWD_A:   # gy[B] in, d[H] in, g[H] out, W2t once (+ dW2 fp32 once: dual kernel)
         return rows * (B + 2 * H) * s + B * H * s + (B * H * 4 if dual_pair_a() else 0)
+    if kind == TIMER_DW_BWD:       # d, g_n2, h1 in, dL/d(hat a1) out
+        return rows * 4 * H * s
+    if kind == TIMER_GEMM_GX:      # g, h1, gy in; dL/dh1, gx out; W1 once
+        return rows * (3 * H + 2 * B) * s + B * H * s
+    if kind == TIMER_COLS_W1:      # dL/dh1, x in (dW1 partials fp32: 32 chunks)
+        return rows * (B + H) * s
+    if kind == TIMER_GEMM2:        # d in, x in (residual), y out; W2 once
+        return rows * (H + 2 * B) * s + B * H * s
     raise ValueError(kind)
+
+
+def copy_peak_gbs(dev, mib=1024, reps=10):
+    """Measured streaming ceiling of this GPU: a device-to-device copy of `mib` MiB
+    (read + write bytes / time, best of `reps`), SURVEY.md §8(d)'s measured peak beside
+    the 8 TB/s datasheet value."""
+    n = mib * (1 << 20) // 4
+    a = torch.empty(n, dtype=torch.float32, device=dev).uniform_()
+    b = torch.empty_like(a)
+    best = float("inf")
+    for _ in range(reps + 2):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        b.copy_(a)
+        e1.record()
+        e1.synchronize()
+        best = min(best, e0.elapsed_time(e1))
+    del a, b
+    return 2 * n * 4 / (best * 1e-3) / 1e9
 
 
 def dual_pair_a():
@@ -253,7 +290,10 @@ def main():
     ap.add_argument("--seconds", type=float, default=None, help="utterance length (config default)")
     ap.add_argument("--fp32", action="store_true", help="fp32 activations (parity mode) instead of bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--timer-kind", type=int, default=TIMER_GEMM_BWD_A)
+    ap.add_argument("--timer-kind", type=int, default=0,
+                    help="kernel timed in the timed region (default: the dominant one of the profile pass)")
+    ap.add_argument("--profile-steps", type=int, default=5,
+                    help="untimed steps with every kernel family timed (the per-kernel table)")
     ap.add_argument("--ddp", action="store_true",
                     help="the data-parallel path over RCCL even at world size 1 (process-group init, "
                          "gradient exchange)")
@@ -352,9 +392,33 @@ def main():
     import ctn_ops
     for _ in range(args.warmup):
         step()
+    lib = L.load()
+    s_el = 4 if args.fp32 else 2
+    # profile pass (untimed): every kernel family bracketed by hipEvents -> per-kernel table
+    table = {}
+    if args.profile_steps > 0:
+        torch.cuda.synchronize(dev)
+        L.check(lib.ctn_timer_enable_mask(sum(1 << k for k in TIMER_NAMES), args.profile_steps * 64),
+                "ctn_timer_enable_mask")
+        for _ in range(args.profile_steps):
+            step()
+        torch.cuda.synchronize(dev)
+        for k in TIMER_NAMES:
+            tk, nk = ctypes.c_double(0.0), ctypes.c_int(0)
+            L.check(lib.ctn_timer_read_kind(k, ctypes.byref(tk), ctypes.byref(nk)), "ctn_timer_read_kind")
+            if nk.value:
+                mean_k = tk.value / nk.value
+                kb_k = kernel_bytes(k, M, K, cfg, s_el)
+                table[k] = {"kernel": TIMER_NAMES[k], "mean_us": round(mean_k * 1e3, 2),
+                            "launches_per_step": round(nk.value / args.profile_steps, 2),
+                            "ms_per_step": round(tk.value / args.profile_steps, 4),
+                            "alg_bytes": kb_k, "GBps": round(kb_k / (mean_k * 1e-3) / 1e9, 1),
+                            "frac": round(kb_k / (mean_k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+        lib.ctn_timer_enable(0, 0)
+    if not args.timer_kind:   # the kernel family with the most time per step
+        args.timer_kind = max(table, key=lambda k: table[k]["ms_per_step"]) if table else TIMER_GEMM_BWD_A
     n_def0 = ctn_ops.DEFERRED_BLOCKS
     torch.cuda.synchronize(dev)
-    lib = L.load()
     L.check(lib.ctn_timer_enable(args.timer_kind, args.steps * 64), "ctn_timer_enable")
     if use_ddp:
         dist.barrier()
@@ -370,6 +434,9 @@ def main():
     nl = ctypes.c_int(0)
     L.check(lib.ctn_timer_read(ctypes.byref(tot), ctypes.byref(nl)), "ctn_timer_read")
     lib.ctn_timer_enable(0, 0)
+    # a generation-word timeout anywhere in the run fails the bench (ctn_device_status)
+    L.check(lib.ctn_device_status(ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream), None, 0),
+            "ctn_device_status")
     rank_ms = [round(elapsed / args.steps * 1e3, 3)]
     if use_ddp:
         # every rank's time (max = the job's time); the list's length is RCCL's world size
@@ -380,9 +447,10 @@ def main():
         elapsed = max(float(x) for x in ts)
     final_loss = float(loss.detach())
     deferred = (ctn_ops.DEFERRED_BLOCKS - n_def0) / args.steps
+    copy_gbs = copy_peak_gbs(dev) if rank == 0 else None
 
     if rank == 0:
-        s = 4 if args.fp32 else 2
+        s = s_el
         ms = elapsed / args.steps * 1e3
         utt_s = world * M * args.steps / elapsed
         kb = kernel_bytes(args.timer_kind, M, K, cfg, s)
@@ -433,17 +501,20 @@ def main():
                        "deferred_grad_reduce_blocks": deferred},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": {1: "gemm_ws fwd 1x1 B->H (PReLU-stats epilogue)",
-                                    2: "dw_fwd (norm1+depthwise+stats)",
-                                    3: ("gemm_dual bwd g_n2 = gy.W2 (norm-backward epilogue) + dW2 = gy^T.n2"
-                                        if dual_pair_a() else
-                                        "gemm_ws bwd g_n2 = gy.W2 (norm-backward epilogue)")}[args.timer_kind],
+                         "kernel": TIMER_NAMES[args.timer_kind] if not (args.timer_kind == TIMER_GEMM_BWD_A and
+                                                                        not dual_pair_a()) else
+                         "gemm_ws bwd g_n2 = gy.W2 (norm-backward epilogue)",
+                         # measured streaming ceiling on this GPU (device copy, read + write)
+                         "copy_peak": round(copy_gbs, 1), "frac_of_copy_peak": round(achieved / copy_gbs, 4),
                          "launches": nl.value, "mean_ms": round(mean_ms, 4), "bytes_per_launch": kb,
                          # rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * 1024 SIMDs) of
                          # this kernel, from the committed PMC pass (profiles/pmc_mfma.json)
                          "mfma_util": mfma.get("mfma_util") if mfma else None,
                          # the whole step against the same peak: SURVEY §8d compulsory bytes
-                         "step_frac": round(step_alg_bytes(M, K, T, cfg, s) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+                         "step_frac": round(step_alg_bytes(M, K, T, cfg, s) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         # every TemporalBlock kernel family, timed live in the untimed profile
+                         # pass (hipEvents on the launch stream), sorted by time per step
+                         "kernels": sorted(table.values(), key=lambda r: -r["ms_per_step"])},
             "step_model": {"alg_bytes_GB": round(step_alg_bytes(M, K, T, cfg, s) / 1e9, 3),
                            "alg_GBps": round(step_alg_bytes(M, K, T, cfg, s) / (ms * 1e-3) / 1e9, 1),
                            "tflops": round(step_flops(M, K, cfg) / (ms * 1e-3) / 1e12, 1),

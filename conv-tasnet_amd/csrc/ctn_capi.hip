@@ -36,55 +36,162 @@ static int fail(int code, const char* fmt, ...) {
 static constexpr double kEps = 1e-8;   // conv_tasnet.py:10
 
 // ---------------------------------------------------------------------------
-// kernel timer (bench.py roofline measurement)
+// kernel timer (bench.py roofline measurement): a set of kernel kinds (CTN_TIMER_*), each
+// launch of a selected kind bracketed by a pair of hipEvents on the launch's stream
 // ---------------------------------------------------------------------------
 namespace {
 struct Timer {
   std::mutex mu;
-  int kind = 0, cap = 0, used = 0;
-  std::vector<hipEvent_t> ev;   // pairs
+  uint32_t mask = 0;
+  int cap = 0;                              // launches per kind
+  int used[32] = {};
+  std::vector<hipEvent_t> ev[32];           // pairs
 };
 Timer g_timer;
 
 struct TimedScope {
   hipStream_t s;
-  int idx = -1;
-  TimedScope(int kind, hipStream_t st) : s(st) {
-    if (g_timer.kind != kind) return;
+  int kind = 0, idx = -1;
+  TimedScope(int k, hipStream_t st) : s(st), kind(k) {
+    if (k <= 0 || k >= 32 || !((g_timer.mask >> k) & 1u)) return;
     std::lock_guard<std::mutex> lk(g_timer.mu);
-    if (g_timer.used >= g_timer.cap) return;
-    idx = g_timer.used++;
-    (void)hipEventRecord(g_timer.ev[2 * idx], s);
+    if (g_timer.used[k] >= g_timer.cap) return;
+    idx = g_timer.used[k]++;
+    (void)hipEventRecord(g_timer.ev[k][2 * idx], s);
   }
   ~TimedScope() {
-    if (idx >= 0) (void)hipEventRecord(g_timer.ev[2 * idx + 1], s);
+    if (idx >= 0) (void)hipEventRecord(g_timer.ev[kind][2 * idx + 1], s);
   }
 };
 }  // namespace
 
-extern "C" int ctn_timer_enable(int kind, int max_launches) {
+extern "C" int ctn_timer_enable_mask(uint32_t mask, int max_launches) {
+  if (max_launches < 0 || (mask & 1u)) return fail(CTN_ERR_ARG, "timer mask 0x%x / launches %d", mask, max_launches);
   std::lock_guard<std::mutex> lk(g_timer.mu);
-  for (auto e : g_timer.ev) (void)hipEventDestroy(e);
-  g_timer.ev.clear();
-  g_timer.kind = kind;
-  g_timer.cap = kind ? max_launches : 0;
-  g_timer.used = 0;
-  g_timer.ev.resize(2 * (size_t)g_timer.cap);
-  for (auto& e : g_timer.ev) CTN_HIP(hipEventCreate(&e));
+  for (int k = 0; k < 32; ++k) {
+    for (auto e : g_timer.ev[k]) (void)hipEventDestroy(e);
+    g_timer.ev[k].clear();
+    g_timer.used[k] = 0;
+  }
+  g_timer.mask = max_launches ? mask : 0u;
+  g_timer.cap = max_launches;
+  for (int k = 1; k < 32; ++k) {
+    if (!((g_timer.mask >> k) & 1u)) continue;
+    g_timer.ev[k].resize(2 * (size_t)g_timer.cap);
+    for (auto& e : g_timer.ev[k]) CTN_HIP(hipEventCreate(&e));
+  }
+  return CTN_OK;
+}
+
+extern "C" int ctn_timer_enable(int kind, int max_launches) {
+  if (kind < 0 || kind >= 32) return fail(CTN_ERR_ARG, "timer kind %d", kind);
+  return ctn_timer_enable_mask(kind ? 1u << kind : 0u, kind ? max_launches : 0);
+}
+
+extern "C" int ctn_timer_read_kind(int kind, double* total_ms, int* launches) {
+  if (kind <= 0 || kind >= 32) return fail(CTN_ERR_ARG, "timer kind %d", kind);
+  std::lock_guard<std::mutex> lk(g_timer.mu);
+  double t = 0.0;
+  for (int i = 0; i < g_timer.used[kind]; ++i) {
+    CTN_HIP(hipEventSynchronize(g_timer.ev[kind][2 * i + 1]));
+    float ms = 0.f;
+    CTN_HIP(hipEventElapsedTime(&ms, g_timer.ev[kind][2 * i], g_timer.ev[kind][2 * i + 1]));
+    t += ms;
+  }
+  if (total_ms) *total_ms = t;
+  if (launches) *launches = g_timer.used[kind];
   return CTN_OK;
 }
 
 extern "C" int ctn_timer_read(double* total_ms, int* launches) {
-  std::lock_guard<std::mutex> lk(g_timer.mu);
   double t = 0.0;
-  for (int i = 0; i < g_timer.used; ++i) {
-    CTN_HIP(hipEventSynchronize(g_timer.ev[2 * i + 1]));
-    float ms = 0.f;
-    CTN_HIP(hipEventElapsedTime(&ms, g_timer.ev[2 * i], g_timer.ev[2 * i + 1]));
-    t += ms;
+  int n = 0;
+  for (int k = 1; k < 32; ++k) {
+    double tk = 0.0;
+    int nk = 0;
+    const int rc = ctn_timer_read_kind(k, &tk, &nk);
+    if (rc) return rc;
+    t += tk;
+    n += nk;
   }
   if (total_ms) *total_ms = t;
-  if (launches) *launches = g_timer.used;
+  if (launches) *launches = n;
+  return CTN_OK;
+}
+
+// ---------------------------------------------------------------------------
+// device error word (ctn_common.h CTN_DEVERR_*): one per device, allocated and zeroed on
+// first use; a pinned host mirror is refreshed asynchronously at the end of every backward
+// pass (ctn_tblock_reduce_grads) and checked at the next one, so a kernel that hit an
+// error fails the call within a step without a device synchronisation on the fast path
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int MAX_DEV = 64;
+struct DevErr {
+  std::mutex mu;
+  uint32_t* word[MAX_DEV] = {};
+  volatile uint32_t* mirror[MAX_DEV] = {};
+};
+DevErr g_deverr;
+
+int dev_err_slot(int* dev) {
+  if (hipGetDevice(dev) != hipSuccess || *dev < 0 || *dev >= MAX_DEV) return -1;
+  std::lock_guard<std::mutex> lk(g_deverr.mu);
+  if (!g_deverr.word[*dev]) {
+    void* w = nullptr;
+    void* h = nullptr;
+    if (hipMalloc(&w, 256) != hipSuccess) return -1;
+    if (hipMemset(w, 0, 256) != hipSuccess || hipHostMalloc(&h, 256, hipHostMallocDefault) != hipSuccess) {
+      (void)hipFree(w);
+      return -1;
+    }
+    *(volatile uint32_t*)h = 0u;
+    g_deverr.mirror[*dev] = (volatile uint32_t*)h;
+    g_deverr.word[*dev] = (uint32_t*)w;
+  }
+  return 0;
+}
+
+const char* dev_err_text(uint32_t w) {
+  return (w & CTN_DEVERR_SPIN) ? "a generation-word wait of a wave-specialised kernel ran out of polls "
+                                      "(CTN_DEVERR_SPIN): that launch's outputs are invalid"
+                                    : "unknown device error bit";
+}
+
+// the mirror of earlier copies (no synchronisation): non-zero once an error has been seen
+int dev_err_check_async() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEV || !g_deverr.mirror[dev]) return CTN_OK;
+  const uint32_t w = *g_deverr.mirror[dev];
+  if (w) return fail(CTN_ERR_HIP, "device error word 0x%x: %s", w, dev_err_text(w));
+  return CTN_OK;
+}
+
+hipError_t dev_err_refresh(hipStream_t s) {
+  int dev = 0;
+  if (dev_err_slot(&dev)) return hipErrorOutOfMemory;
+  return hipMemcpyAsync((void*)g_deverr.mirror[dev], g_deverr.word[dev], 4, hipMemcpyDeviceToHost, s);
+}
+}  // namespace
+
+uint32_t* ctn::device_error_word() {
+  int dev = 0;
+  return dev_err_slot(&dev) ? nullptr : g_deverr.word[dev];
+}
+
+extern "C" int ctn_device_status(void* stream, uint32_t* word, int clear) {
+  int dev = 0;
+  if (dev_err_slot(&dev)) return fail(CTN_ERR_HIP, "device error word: allocation failed");
+  hipStream_t s = (hipStream_t)stream;
+  uint32_t w = 0;
+  CTN_HIP(hipStreamSynchronize(s));
+  CTN_HIP(hipMemcpy(&w, g_deverr.word[dev], 4, hipMemcpyDeviceToHost));
+  if (clear && w) {
+    CTN_HIP(hipMemset(g_deverr.word[dev], 0, 4));
+    *g_deverr.mirror[dev] = 0u;
+  }
+  if (word) *word = w;
+  if (w) return fail(CTN_ERR_HIP, "device error word 0x%x: %s", w, dev_err_text(w));
   return CTN_OK;
 }
 
@@ -611,7 +718,7 @@ extern "C" int ctn_tblock_forward(const ctn_tblock_desc* d, const ctn_tblock_par
     g1.eps = (float)kEps;
   }
   {
-    TimedScope ts(1, s);
+    TimedScope ts(CTN_TIMER_GEMM1, s);
     CTN_HIP(launch_gemm_rows(dt, g1, s));
   }
   // gLN: the consumers finalize the statistics from the slab partials (StatFold)
@@ -630,7 +737,7 @@ extern "C" int ctn_tblock_forward(const ctn_tblock_desc* d, const ctn_tblock_par
     da.eps = (float)kEps;
   }
   {
-    TimedScope ts(2, s);
+    TimedScope ts(CTN_TIMER_DW_FWD, s);
     CTN_HIP(launch_dw_fwd(dt, da, s));
   }
   // norm2 apply (+PReLU) on the operand, 1x1 conv H->B, residual add
@@ -645,7 +752,10 @@ extern "C" int ctn_tblock_forward(const ctn_tblock_desc* d, const ctn_tblock_par
   if (fold && (ws_fold_mask() & 1) && gemm_ws_can_fold(dt, g2))
     g2.aop.fold = StatFold{L.slab2, L.parts2, cnt, (float)kEps, 0, st2};
   else if (!da.st2_out) CTN_HIP(launch_stats_finalize(L.slab2, G, L.parts2, cnt, 0, (float)kEps, st2, s));
-  CTN_HIP(launch_gemm_rows(dt, g2, s));
+  {
+    TimedScope ts(CTN_TIMER_GEMM2, s);
+    CTN_HIP(launch_gemm_rows(dt, g2, s));
+  }
   return CTN_OK;
 }
 
@@ -762,11 +872,11 @@ static int tb_backward(const ctn_tblock_desc* d, const ctn_tblock_params* p, con
   duA.Dpart = L.cpart2;
   const bool dualA = gemm_dual_eligible(dt, duA);
   if (dualA) {
-    TimedScope ts(3, s);
+    TimedScope ts(CTN_TIMER_GEMM_A, s);
     CTN_HIP(launch_gemm_dual(duA, s));
   } else {
     {
-      TimedScope ts(3, s);
+      TimedScope ts(CTN_TIMER_GEMM_A, s);
       CTN_HIP(launch_gemm_rows(dt, ga, s));
     }
     GemmCols c2{};
@@ -794,7 +904,10 @@ static int tb_backward(const ctn_tblock_desc* d, const ctn_tblock_params* p, con
                      : gemm_rows_stat_fold(dt, ga, L.slabA, cnt, 0.f, 1, nullptr);
   else
     da.sm1_out = L.sums1;   // cLN: per-row norm-1 backward means final in the depthwise kernel
-  CTN_HIP(launch_dw_bwd(dt, da, s));
+  {
+    TimedScope ts(CTN_TIMER_DW_BWD, s);
+    CTN_HIP(launch_dw_bwd(dt, da, s));
+  }
   const bool fused1 = tb_fused_n1(d);
   int nalpha = ew_blocks(da);
   if (fused1) {
@@ -812,7 +925,10 @@ static int tb_backward(const ctn_tblock_desc* d, const ctn_tblock_params* p, con
       if (fold) CTN_HIP(launch_stats_finalize(L.slabD, G, L.partsD, cnt, 1, 0.f, L.sums1, s));
       gb.aop.sums = L.sums1;
     }
-    CTN_HIP(launch_gemm_rows(dt, gb, s));
+    {
+      TimedScope ts(CTN_TIMER_GEMM_GX, s);
+      CTN_HIP(launch_gemm_rows(dt, gb, s));
+    }
     nalpha = gemm_ws_grid(gb);
     // everything below only produces parameter gradients: fork to sw
     if (sw != s) CTN_HIP(fork_stream(s, sw));
@@ -822,7 +938,10 @@ static int tb_backward(const ctn_tblock_desc* d, const ctn_tblock_params* p, con
     c1.A = L.G1; c1.lda = d->H;
     c1.B = x; c1.ldb = d->B;
     c1.Cpart = L.cpart1; c1.nchunks = L.chunks1;
-    CTN_HIP(launch_gemm_cols(dt, c1, sw));
+    {
+      TimedScope ts(CTN_TIMER_COLS_W1, sw);
+      CTN_HIP(launch_gemm_cols(dt, c1, sw));
+    }
   } else {
     // (d) norm1 backward finish + PReLU1 backward -> G1 = dL/dh1
     DwArgs de = da;
@@ -884,6 +1003,8 @@ extern "C" int ctn_tblock_backward_deferred(const ctn_tblock_desc* d, const ctn_
 extern "C" int ctn_tblock_reduce_grads(const ctn_tblock_desc* descs, const ctn_tblock_grads* grads,
                                        void* const* parts, int n, void* stream) {
   if (n < 0 || (n > 0 && (!descs || !grads || !parts))) return fail(CTN_ERR_ARG, "null pointer");
+  // an error a kernel of an earlier pass reported (device error word, copied asynchronously)
+  if (int rc = dev_err_check_async()) return rc;
   std::vector<SlabDesc> sd;
   std::vector<float*> tmp;
   sd.reserve((size_t)n * 9);
@@ -905,6 +1026,7 @@ extern "C" int ctn_tblock_reduce_grads(const ctn_tblock_desc* descs, const ctn_t
     }
   }
   CTN_HIP(launch_slab_reduce_list(sd.data(), tmp.data(), (int)sd.size(), (hipStream_t)stream));
+  CTN_HIP(dev_err_refresh((hipStream_t)stream));   // checked by the next pass (or ctn_device_status)
   return CTN_OK;
 }
 

@@ -89,16 +89,30 @@ CTN_DEV void lds_barrier() {
 // Generation words in LDS (ring hand-offs between waves of one workgroup, no barrier):
 // a wave publishes `gen` in its word of a slot after its own LDS operations on the slot
 // completed (flag_signal), and a consumer polls the N words of a slot until all reach
-// `gen` (flag_wait; wave-uniform by readfirstlane, bounded at ~0.2 s so a protocol
-// error ends the launch with wrong results instead of a wave that never finishes).
+// `gen` (flag_wait; wave-uniform by readfirstlane).  The poll is bounded (CTN_SPIN_LIMIT
+// polls, ~0.2 s) so that a protocol error cannot leave a wave spinning forever; when the
+// bound runs out the wave sets CTN_DEVERR_SPIN in the device error word `err` (one vector
+// atomic by lane 0) and goes on, and the host reports the launch as failed
+// (ctn_device_status, ctn_tblock_reduce_grads: CTN_ERR_HIP) instead of returning its
+// wrong results silently.
 // Volatile accesses keep their address space only through an LDS-typed pointer (a
 // generic one becomes a FLAT access, whose wait drains every outstanding global load).
+#ifndef CTN_SPIN_LIMIT
+#define CTN_SPIN_LIMIT (1u << 22)
+#endif
+#ifndef CTN_DEVERR_SPIN
+#define CTN_DEVERR_SPIN 1u   // a generation-word wait timed out (include/ctn.h)
+#endif
+CTN_DEV void spin_timeout(uint32_t* err) {
+  if (err && (threadIdx.x & 63) == 0) atomicOr(err, CTN_DEVERR_SPIN);
+}
 typedef __attribute__((address_space(3))) volatile v4u flag_v4u;
 typedef __attribute__((address_space(3))) volatile uint32_t flag_u32;
-template <int N> CTN_DEV void flag_wait(const uint32_t* f, uint32_t gen) {
+template <int N> CTN_DEV void flag_wait(const uint32_t* f, uint32_t gen, uint32_t* err) {
   static_assert(N % 4 == 0, "generation words per slot: whole 16-byte reads");
   const flag_v4u* fl = (const flag_v4u*)(f);
-  for (uint32_t it = 0; it < (1u << 22); ++it) {
+  uint32_t it = 0;
+  for (; it < CTN_SPIN_LIMIT; ++it) {
     uint32_t mn = 0xffffffffu;
 #pragma unroll
     for (int i = 0; i < N / 4; ++i) {
@@ -108,6 +122,7 @@ template <int N> CTN_DEV void flag_wait(const uint32_t* f, uint32_t gen) {
     if (__builtin_amdgcn_readfirstlane(mn) >= gen) break;
     __builtin_amdgcn_s_sleep(1);
   }
+  if (it == CTN_SPIN_LIMIT) spin_timeout(err);
   asm volatile("" ::: "memory");
 }
 CTN_DEV void flag_signal(uint32_t* f, uint32_t gen) {

@@ -171,17 +171,19 @@ CTN_DEV s16x4_t dv_tr(const char* p) {
 // the poll is followed by a compiler barrier so no LDS read of the published data is
 // issued before the word that publishes it has been seen (LDS executes one wave's
 // DS instructions in order).
-// The spin is bounded (about 0.2 s): a protocol error ends the launch with wrong
-// results instead of a wave that never finishes.
+// The spin is bounded (CTN_SPIN_LIMIT polls, about 0.2 s): a protocol error sets
+// CTN_DEVERR_SPIN in the device error word (p.err, ctn_device_status) and the launch
+// ends, reported as failed by the host, instead of a wave that never finishes.
 // (Volatile accesses keep their address space only through an explicitly LDS-typed
 // pointer: through a generic one they become FLAT operations, whose waits drain every
 // outstanding global load of the wave.)
 typedef __attribute__((address_space(3))) volatile v4u lds_v4u;
 typedef __attribute__((address_space(3))) volatile uint32_t lds_u32;
-template <int N> CTN_DEV void dv_wait(const uint32_t* f, uint32_t gen) {
+template <int N> CTN_DEV void dv_wait(const uint32_t* f, uint32_t gen, uint32_t* err) {
   static_assert(N % 4 == 0, "generation words per slot: whole 16-byte reads");
   const lds_v4u* fl = (const lds_v4u*)(f);
-  for (uint32_t it = 0; it < (1u << 22); ++it) {
+  uint32_t it = 0;
+  for (; it < CTN_SPIN_LIMIT; ++it) {
     uint32_t mn = 0xffffffffu;
 #pragma unroll
     for (int i = 0; i < N / 4; ++i) {
@@ -191,6 +193,7 @@ template <int N> CTN_DEV void dv_wait(const uint32_t* f, uint32_t gen) {
     if (__builtin_amdgcn_readfirstlane(mn) >= gen) break;
     __builtin_amdgcn_s_sleep(1);
   }
+  if (it == CTN_SPIN_LIMIT) spin_timeout(err);
   asm volatile("" ::: "memory");
 }
 // publish: this wave's LDS writes (and reads) complete, then the generation word
@@ -298,7 +301,7 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
       int slot = 0;
       uint32_t gen = 1;
       for (int t = t0; t < t1; ++t) {
-        dv_wait<4>(fl_full[slot], gen);
+        dv_wait<4>(fl_full[slot], gen, p.err);
         char* base = smem + slot * SLOT;
         if constexpr (CTN_DV_EXP & 16) {   // C stores only (zeros)
 #pragma unroll
@@ -443,7 +446,7 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
       int slot = 0;
       uint32_t gen = 1;
       for (int t = t0; t < t1; ++t) {
-        dv_wait<4>(fl_full[slot], gen);
+        dv_wait<4>(fl_full[slot], gen, p.err);
         const char* base = smem + slot * SLOT;
         if constexpr (!(CTN_DV_EXP & 3)) {
           const char* a = base + OFF_A;
@@ -643,7 +646,7 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
       const int tn = t + PF;
       if (tn < t1) {
         const int kn = tn - t0;   // its slot was last used by tile tn - NSL: wait for every DONE of it
-        dv_wait<ND>(fl_done[kn % NSL], (uint32_t)(kn / NSL));
+        dv_wait<ND>(fl_done[kn % NSL], (uint32_t)(kn / NSL), p.err);
         dma(tn);
       }
       if (++slot == NSL) {
@@ -718,6 +721,7 @@ int gemm_cols_ws_ranges(const GemmCols& c) {
 
 hipError_t launch_gemm_cols_ws(const GemmCols& c, hipStream_t s) {
   GemmDual p{};
+  p.err = device_error_word();
   p.g = c.g;
   p.Kred = c.Q;
   p.Nout = c.P;
@@ -730,8 +734,10 @@ hipError_t launch_gemm_cols_ws(const GemmCols& c, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_gemm_dual_ws(const GemmDual& p, hipStream_t s) {
-  if (!gemm_dual_ws_eligible(p)) return hipErrorInvalidValue;
+hipError_t launch_gemm_dual_ws(const GemmDual& pa, hipStream_t s) {
+  if (!gemm_dual_ws_eligible(pa)) return hipErrorInvalidValue;
+  GemmDual p = pa;
+  p.err = device_error_word();
   const dim3 grid(gemm_dual_ws_ranges(p) * (p.Nout / DV_NS));
   if (p.norm == NORM_GLN)
     hipLaunchKernelGGL((gemm_dual_ws_kernel<NORM_GLN, DV_NSL, DV_PF>), grid, dim3(DV_NT), 0, s, p);

@@ -686,13 +686,13 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
           const int slot = t % WS_DR;
           const uint32_t gen = (uint32_t)((t - t0) / WS_DR + 1);
           flag_signal(&fl_full[slot][wid], gen);   // this wave's DMA of tile t landed
-          flag_wait<WV>(fl_full[slot], gen);       // every wave's
+          flag_wait<WV>(fl_full[slot], gen, p.err);       // every wave's
           mfma_tile(sA[slot], acc);
           if constexpr (!(CTN_WS_EXP & 64)) __builtin_amdgcn_sched_barrier(0);
           flag_signal(&fl_done[slot][wid], gen);   // this wave's reads of the slot done
           const int tn = t + WS_DR - 1;            // into the slot of tile t - 1
           if (tn < t1) {
-            if (t > t0) flag_wait<WV>(fl_done[(t - 1) % WS_DR], (uint32_t)((t - 1 - t0) / WS_DR + 1));
+            if (t > t0) flag_wait<WV>(fl_done[(t - 1) % WS_DR], (uint32_t)((t - 1 - t0) / WS_DR + 1), p.err);
             dma(tn);
           }
           epilogue_math(le1, t, acc);
@@ -949,7 +949,9 @@ static hipError_t ws_launch_nk(const GemmRows& p, hipStream_t s) {
   }
 }
 
-hipError_t launch_gemm_ws(const GemmRows& p, hipStream_t s) {
+hipError_t launch_gemm_ws(const GemmRows& pa, hipStream_t s) {
+  GemmRows p = pa;
+  p.err = device_error_word();   // the generation-word ring (CTN_WS_FLAGS) reports timeouts here
   const int nk = p.aop.kind != OP_PLAIN ? p.aop.norm : p.norm;
   return nk == NORM_GLN ? ws_launch_nk<NORM_GLN>(p, s) : ws_launch_nk<NORM_CLN>(p, s);
 }

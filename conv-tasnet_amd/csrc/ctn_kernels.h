@@ -10,6 +10,11 @@
 namespace ctn {
 
 enum DType { F32 = 0, BF16 = 1 };
+
+// The current device's error word (ctn_capi.hip: allocated and zeroed on first use, read by
+// ctn_device_status / ctn_tblock_reduce_grads).  Kernels whose waves hand tiles to each
+// other through LDS generation words set CTN_DEVERR_SPIN in it when a wait runs out.
+uint32_t* device_error_word();
 // OP_NORM1_BWD (bf16, gLN; WS kernel, the first 1x1's data gradient): the operand
 // is g = dL/d(hat a1) and becomes dL/dh1 = PReLU'(h1) * rstd * (g - mean g - hat a1 *
 // mean(g hat a1)) on the way into LDS (conv_tasnet.py:217-219 backward), with
@@ -63,6 +68,7 @@ struct GemmRows {
   // output written here directly (the workgroup holds every channel of its rows)
   float2* stats_out = nullptr;
   float eps = 0.f;
+  uint32_t* err = nullptr;                // device error word (ring hand-off timeouts), set by the launcher
 };
 // Slab sizing must be queried with the same GemmRows (shape, operand op, epilogue,
 // strides) that is later launched: the kernel choice decides the part counts.
@@ -112,6 +118,7 @@ struct GemmDual {
   const void* Bm; int ldb;
   RowOp bop;                   // OP_PLAIN or OP_PRELU_NORM with final statistics
   float* Dpart;                // [gemm_dual_ranges][Kred][Nout]
+  uint32_t* err = nullptr;     // device error word (generation-word timeouts), set by the launcher
 };
 bool gemm_dual_eligible(DType dt, const GemmDual& p);
 int gemm_dual_ranges(const GemmDual& p);
@@ -216,10 +223,16 @@ int dw_seg(const DwArgs& a, bool bwd);   // comb segment length sizing one resid
 int dw_blocks(const DwArgs& a);        // depthwise (comb) kernels (a.seg set)
 int ew_blocks(const DwArgs& a);        // norm1_bwd (128-row blocks)
 int dw_parts_per_group(const DwArgs& a);   // slab parts per utterance (gLN) or per row (cLN)
-__host__ __device__ int dw_col_stride(const DwArgs& a);
+// col_slab part layout: [ggamma1 H][gbeta1 H][gwd H*P][ggamma2 H][gbeta2 H][galpha2 1], padded to 4
+__host__ __device__ inline int dw_col_stride(const DwArgs& a) { return ((4 + a.P) * a.H + 1 + 3) & ~3; }
 hipError_t launch_dw_fwd(DType dt, const DwArgs& a, hipStream_t s);
 hipError_t launch_dw_bwd(DType dt, const DwArgs& a, hipStream_t s);
 hipError_t launch_norm1_bwd(DType dt, const DwArgs& a, hipStream_t s);
+// wave-item forms (ctn_dw_wave.hip: bf16, H = 512, P = 3), chosen by launch_dw_fwd / _bwd;
+// CTN_DW_WAVE=0 keeps the lane-group kernels
+bool dw_wave_eligible(DType dt, const DwArgs& a);
+hipError_t launch_dw_fwd_wave(const DwArgs& a, hipStream_t s);
+hipError_t launch_dw_bwd_wave(const DwArgs& a, hipStream_t s);
 
 // ---- stand-alone separator layers on frame rows (ctn_layers.hip) ------------
 enum LayerOp {

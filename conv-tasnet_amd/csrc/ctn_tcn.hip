@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "ctn_common.h"
+#include "ctn_dw.h"
 #include "ctn_kernels.h"
 
 namespace ctn {
@@ -35,29 +36,6 @@ constexpr int DW_WPS_FWD = 4, DW_WPS_BWD = 2;   // waves/SIMD the kernels' VGPR 
 // in flight: 8 waves x 48 B per lane per CU is half of what Little's law asks at
 // 6 TB/s), 1 for fp32 (parity mode; two would exceed the VGPR budgets above)
 template <typename T> constexpr int dw_pf() { return sizeof(T) == 2 ? CTN_DW_PF : 1; }
-
-// ---------------------------------------------------------------------------
-// Comb decomposition of the dilated depthwise conv.  Rows of one utterance are
-// split into residue classes rho mod d; a work item walks rows rho + j*d for
-// j in one segment of a.seg steps (dw_seg).  A lane group of H/8 lanes owns one item and
-// all H channels of its rows (8 per lane, 16-byte vectors); the P taps of a
-// row are consecutive comb steps, so they live in a sliding register window:
-// every row is loaded and transformed once (plus P-1 halo rows per segment)
-// and the next row is prefetched while the current one is computed.
-// ---------------------------------------------------------------------------
-struct CombGeom {
-  int cg, ipw, jmax, nseg, items, wgpu;
-};
-__host__ __device__ inline CombGeom comb_geom(const DwArgs& a) {
-  CombGeom g;
-  g.cg = a.H / 8;
-  g.ipw = 4 * (64 / g.cg);
-  g.jmax = (a.g.Kp + a.dil - 1) / a.dil;
-  g.nseg = (g.jmax + a.seg - 1) / a.seg;
-  g.items = a.dil * g.nseg;
-  g.wgpu = (g.items + g.ipw - 1) / g.ipw;
-  return g;
-}
 
 // Segment length such that all work items of the launch are resident at once:
 // a wave owns 64/(H/8) items and walks its segment serially, so a second, partly
@@ -84,36 +62,9 @@ int dw_seg(const DwArgs& a, bool bwd) {
 int dw_blocks(const DwArgs& a) { return a.g.M * comb_geom(a).wgpu; }
 int dw_parts_per_group(const DwArgs& a) { return a.norm == NORM_GLN ? comb_geom(a).wgpu : 1; }
 int ew_blocks(const DwArgs& a) { return (int)(a.g.rows() / DW_RPB); }
-// col_slab part layout: [ggamma1 H][gbeta1 H][gwd H*P][ggamma2 H][gbeta2 H][galpha2 1], padded to 4
-__host__ __device__ int dw_col_stride(const DwArgs& a) { return ((4 + a.P) * a.H + 1 + 3) & ~3; }
 
 template <int NK> CTN_DEV float2 ld_stat(const float2* s, int m, int row) {
   return NK == NORM_GLN ? s[m] : s[row];
-}
-
-// cLN per-row sums of a comb walk.  With H = 512 one wave owns one comb item (its 64
-// lanes hold all channels of each row), so a row's sums are reduced with DPP (no LDS
-// round trips), parked one row per lane, and every 64 rows each lane finishes the row
-// it holds: the fp64 finishing arithmetic runs once per 64 rows, not once per row.
-// Narrower H (several items per wave) reduces per row over the lane group as before.
-struct RowPark {
-  float s = 0.f, ss = 0.f;
-  int j0;   // comb step held by lane 0
-};
-
-// column-partial reduction: sum val[8] over the lanes that own channel group c, write H floats
-CTN_DEV void col_reduce8(float* buf, const float v[8], int rl, int c, int nrl, int cg, bool act, float* dst) {
-  const int H = cg * 8;
-  if (act)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) buf[rl * H + c * 8 + e] = v[e];
-  __syncthreads();
-  for (int ch = threadIdx.x; ch < H; ch += blockDim.x) {
-    float s = 0.f;
-    for (int q = 0; q < nrl; ++q) s += buf[q * H + ch];
-    dst[ch] = s;
-  }
-  __syncthreads();
 }
 
 struct CombItem {
@@ -679,6 +630,7 @@ static hipError_t dw_check(const DwArgs& a) {
   hipError_t launch_##NAME(DType dt, const DwArgs& a, hipStream_t s) {                       \
     hipError_t e = dw_check(a);                                                              \
     if (e != hipSuccess) return e;                                                           \
+    if (dw_wave_eligible(dt, a)) return launch_##NAME##_wave(a, s);                           \
     if (dt == BF16)                                                                          \
       return a.norm == NORM_GLN ? NAME##_dispatch_p<bf16raw, NORM_GLN>(a, s)                 \
                                 : NAME##_dispatch_p<bf16raw, NORM_CLN>(a, s);                \
@@ -713,6 +665,7 @@ static hipError_t dw_bwd_dispatch_p(const DwArgs& a, hipStream_t s) {
 hipError_t launch_dw_bwd(DType dt, const DwArgs& a, hipStream_t s) {
   hipError_t e = dw_check(a);
   if (e != hipSuccess) return e;
+  if (dw_wave_eligible(dt, a)) return launch_dw_bwd_wave(a, s);
   if (dt == BF16)
     return a.norm == NORM_GLN ? dw_bwd_dispatch_p<bf16raw, NORM_GLN>(a, s) : dw_bwd_dispatch_p<bf16raw, NORM_CLN>(a, s);
   return a.norm == NORM_GLN ? dw_bwd_dispatch_p<float, NORM_GLN>(a, s) : dw_bwd_dispatch_p<float, NORM_CLN>(a, s);

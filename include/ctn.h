@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define CTN_ABI_VERSION 8
+#define CTN_ABI_VERSION 9
 
 typedef enum { CTN_DTYPE_F32 = 0, CTN_DTYPE_BF16 = 1 } ctn_dtype;
 /* CTN_NORM_BN: torch.nn.BatchNorm1d, chose_norm's fallback branch (conv_tasnet.py:302-303) */
@@ -379,13 +379,38 @@ int ctn_stream_call(const ctn_stream_desc* d, const ctn_stream_model* model, int
                     size_t ws_bytes, void* stream);
 
 /* -------------------------------------------------------------------------
- * Opt-in kernel timer (bench.py roofline): when enabled, every launch of the
- * selected kernel family is bracketed by hipEvents on its stream.
- * kind: 0 off, 1 block-forward first 1x1 GEMM, 2 depthwise forward,
- *       3 block-backward data GEMM (norm-backward epilogue)
+ * Opt-in kernel timer (bench.py roofline; the reference has no counterpart — its
+ * solver prints epoch wall time only, src/solver.py:178-188): when enabled, every
+ * launch of a selected kernel family is bracketed by hipEvents on its stream.
+ * Kinds of the TemporalBlock (conv_tasnet.py:212-272):
  * ------------------------------------------------------------------------- */
+enum {
+  CTN_TIMER_GEMM1 = 1,     /* forward first 1x1 (B -> H, PReLU-statistics epilogue)       */
+  CTN_TIMER_DW_FWD = 2,    /* depthwise forward (norm 1 applied, PReLU-2 statistics)      */
+  CTN_TIMER_GEMM_A = 3,    /* backward pair A: g_n2 = gy.W2 (+ dW2 on the dual kernel)     */
+  CTN_TIMER_DW_BWD = 4,    /* depthwise backward (norm-2 / PReLU-2 backward, dW_dw, sums)  */
+  CTN_TIMER_GEMM_GX = 5,   /* backward gx = n1bwd(g).W1 + gy (stores dL/dh1)              */
+  CTN_TIMER_COLS_W1 = 6,   /* backward dW1 = (dL/dh1)^T . x column GEMM                   */
+  CTN_TIMER_GEMM2 = 7      /* forward second 1x1 (H -> B, norm 2 applied, residual)       */
+};
+/* one kind (0 = off), or a set of kinds (bit k = kind k; max_launches per kind) */
 int ctn_timer_enable(int kind, int max_launches);
-int ctn_timer_read(double* total_ms, int* launches);
+int ctn_timer_enable_mask(uint32_t mask, int max_launches);
+int ctn_timer_read(double* total_ms, int* launches);              /* all kinds */
+int ctn_timer_read_kind(int kind, double* total_ms, int* launches);
+
+/* -------------------------------------------------------------------------
+ * Device error word (ABI v9).  Kernels whose waves hand tiles to each other through
+ * LDS generation words (the wave-specialised dual GEMM of ctn_tblock_backward*, the
+ * ring variant of the weight-stationary GEMM) bound every wait; a wait that runs out
+ * sets bit CTN_DEVERR_SPIN and the launch's outputs are invalid.  The word is copied
+ * to the host asynchronously at the end of every ctn_tblock_reduce_grads, which fails
+ * with CTN_ERR_HIP at its next call once a bit is set.  ctn_device_status
+ * synchronises `stream`, returns the word in *word (may be NULL) and CTN_ERR_HIP when
+ * it is non-zero; clear != 0 resets it.
+ * ------------------------------------------------------------------------- */
+#define CTN_DEVERR_SPIN 1u
+int ctn_device_status(void* stream, uint32_t* word, int clear);
 
 #ifdef __cplusplus
 }
