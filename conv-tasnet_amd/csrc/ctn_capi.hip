@@ -8,6 +8,7 @@
 #include <string.h>
 
 #include <mutex>
+#include <string>
 #include <vector>
 
 #include "../../include/ctn.h"
@@ -982,6 +983,48 @@ static int tb_backward(const ctn_tblock_desc* d, const ctn_tblock_params* p, con
   return CTN_OK;
 }
 
+// Which kernel each step of the block would launch (ctn_tblock_plan): the eligibility
+// queries the launches themselves make, on the descriptor alone
+extern "C" int ctn_tblock_plan(const ctn_tblock_desc* d, int backward, char* out, size_t cap) {
+  int rc = tb_check(d);
+  if (rc) return rc;
+  if (!out || cap < 1) return fail(CTN_ERR_ARG, "null output");
+  const DType dt = tb_dt(d);
+  std::string s;
+  DwArgs da{};
+  da.g = Rows{d->M, d->K, d->Kp}; da.H = d->H; da.P = d->P; da.dil = d->dilation; da.pad = tb_pad(d);
+  da.norm = d->norm_type;
+  if (d->norm_type == CTN_NORM_BN) {
+    s = backward ? "bn:rows+cols" : "bn:rows";
+  } else if (!backward) {
+    GemmRows g2{};
+    g2.g = da.g; g2.Kred = d->H; g2.Nout = d->B; g2.norm = d->norm_type; g2.lda = d->H; g2.ldw = d->H;
+    g2.aop.kind = OP_PRELU_NORM; g2.aop.norm = d->norm_type; g2.epi = EPI_RESID; g2.ldr = d->B; g2.ldc = d->B;
+    da.seg = dw_seg(da, false);
+    s = std::string("gemm1=") + (gemm_ws_eligible(dt, tb_gemm1(d)) ? "ws" : "rows") +
+        ",dw_fwd=" + (dw_wave_eligible(dt, da) ? "wave" : "lane") +
+        ",gemm2=" + (gemm_ws_eligible(dt, g2) ? "ws" : "rows");
+  } else {
+    const GemmDual duA = tb_dualA(d), duB = tb_dualB(d);
+    da.seg = dw_seg(da, true);
+    const bool dualA = gemm_dual_eligible(dt, duA);
+    s = std::string("pairA=") + (dualA ? (gemm_dual_ws_eligible(duA) ? "dual_ws" : "dual")
+                                       : (gemm_ws_eligible(dt, tb_gemmA(d)) ? "ws+cols" : "rows+cols")) +
+        ",dw_bwd=" + (dw_wave_eligible(dt, da) ? "wave" : "lane");
+    if (tb_fused_n1(d)) {
+      GemmCols c1{};
+      c1.g = da.g; c1.P = d->H; c1.Q = d->B; c1.lda = d->H; c1.ldb = d->B;
+      c1.A = c1.B = c1.Cpart = reinterpret_cast<float*>(256);   // alignment only
+      s += std::string(",gx=ws_n1bwd,dW1=") + (gemm_cols_ws_eligible(dt, c1) ? "cols_ws" : "cols");
+    } else {
+      s += std::string(",n1bwd=ew,gx+dW1=") + (gemm_dual_eligible(dt, duB) ? "dual" : "rows+cols");
+    }
+  }
+  if (s.size() + 1 > cap) return fail(CTN_ERR_ARG, "plan needs %zu bytes", s.size() + 1);
+  memcpy(out, s.c_str(), s.size() + 1);
+  return CTN_OK;
+}
+
 extern "C" size_t ctn_tblock_partials_bytes(const ctn_tblock_desc* d) {
   if (tb_check(d) != CTN_OK || d->norm_type == CTN_NORM_BN) return 0;
   return tb_layout(d, 1, nullptr, nullptr, true).part_bytes;
@@ -1883,6 +1926,9 @@ hipGraphExec_t stream_graph_find(const std::vector<uintptr_t>& key) {
 void stream_graph_store(const std::vector<uintptr_t>& key, hipGraphExec_t exec) {
   std::lock_guard<std::mutex> lk(g_sg_mu);
   if (g_sg.size() == 8) {
+    // the evicted graph may still be running on some stream: let the device finish it
+    // first (rare: a ninth distinct argument set)
+    (void)hipDeviceSynchronize();
     (void)hipGraphExecDestroy(g_sg.front().exec);
     g_sg.erase(g_sg.begin());
   }

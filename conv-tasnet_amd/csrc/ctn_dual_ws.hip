@@ -686,6 +686,9 @@ bool gemm_dual_ws_eligible(const GemmDual& p) {
   if (p.bop.norm != p.norm || p.stats != p.bop.stats || p.bop.fold.slab) return false;
   if (p.g.Kp % DV_TM || p.lda % 8 || p.ldb % 8 || p.ldc % 8 || p.ldw % 8) return false;
   if (p.g.rows() / DV_TM < 1) return false;
+  // 32-bit tile offsets and buffer sizes (du_rsrc clamps at 2^31 bytes): larger tensors
+  // take the tiled kernels
+  if (p.g.rows() * (p.Kred > p.Nout ? p.Kred : p.Nout) * 2 >= (1L << 31)) return false;
   const int S = p.Nout / DV_NS;
   return DV_GRID % S == 0;
 }
@@ -709,6 +712,7 @@ bool gemm_cols_ws_eligible(DType dt, const GemmCols& c) {
   if (dt != BF16 || c.aop.kind != OP_PLAIN || c.bop.kind != OP_PLAIN) return false;
   if (c.Q != DV_KR || c.P % DV_NS || DV_GRID % (c.P / DV_NS)) return false;
   if (c.g.Kp % DV_TM || c.lda % 8 || c.ldb % 8 || c.g.rows() / DV_TM < 1) return false;
+  if (c.g.rows() * (c.P > c.Q ? c.P : c.Q) * 2 >= (1L << 31)) return false;   // 32-bit offsets
   if (((uintptr_t)c.A | (uintptr_t)c.B | (uintptr_t)c.Cpart) & 15) return false;
   return true;
 }

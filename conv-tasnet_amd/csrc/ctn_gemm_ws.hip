@@ -851,6 +851,8 @@ bool gemm_ws_eligible(DType dt, const GemmRows& p) {
   int nb, kb;
   if (dt != BF16 || !ws_enabled() || !ws_shape(p.Nout, p.Kred, &nb, &kb) || !ws_pair(p.aop.kind, p.epi)) return false;
   if (p.g.Kp % WS_TM || p.lda % 8 || p.ldw % 8 || p.ldc % 8) return false;
+  // 32-bit tile offsets and buffer sizes (the LDS-DMA ring's du_rsrc clamps at 2^31 bytes)
+  if (p.g.rows() * (p.Kred > p.Nout ? p.Kred : p.Nout) * 2 >= (1L << 31)) return false;
   if ((p.epi == EPI_RESID || p.epi == EPI_NORM_BWD) && p.ldr % 8) return false;
   if (p.aop.kind != OP_PLAIN && p.aop.norm == NORM_GLN && p.g.M > WS_FOLD_MAX) return false;
   if (p.aop.kind == OP_NORM1_BWD && (!p.aop.aux || !p.aop.aout || !p.aop.apart || !p.aop.stats ||

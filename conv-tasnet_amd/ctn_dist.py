@@ -8,12 +8,23 @@ replica and its shard of the global batch, and the gradients are averaged across
 before clip + Adam.  DistributedDataParallel does that with hooks that read each
 gradient as it arrives during backward, which forces every TemporalBlock backward to
 write its parameter gradients immediately (68 reduction launches per step at the bench
-shape) instead of the one batched reduction at the end of the pass
+shape) instead of the batched reductions of the deferred path
 (ConvTasNet.defer_grad_reduce, ctn_ops._end_of_backward).  ``FlatGradAllReduce``
-consumes the gradients only after ``backward()`` returns, so the deferred reductions
-stay on and write straight into its persistent gradient buffer, and exchanges that
-buffer with ONE all-reduce per dtype: one ring all-reduce of the whole model (≈35 MB fp32 for the paper configuration) — a single large message is what
-point-to-point xGMI rings move at full link rate.
+owns one persistent gradient buffer in which every parameter has a view; the deferred
+block backwards write their gradients straight into it.
+
+Chunked exchange (default 4 chunks): the deferred blocks are reduced in groups during
+the backward pass (ctn_ops exchange hook: every ``group_blocks`` block backwards), and
+each group's contiguous slice of the buffer is all-reduced asynchronously (RCCL's own
+stream) as soon as it is final, while the backward of the earlier blocks goes on; what
+is left when ``backward()`` returns (the first blocks, the encoder, bottleneck, mask and
+decoder gradients) is one more all-reduce in :meth:`sync`.  The layout is learnt in the
+first step, in which every deferred block is reduced and reported on its own: the
+reported blocks in report order, split into ``chunks - 1`` groups of consecutive blocks,
+then everything else, so every chunk is one contiguous message (at the paper
+configuration 4 messages of ≈8.7 MB, still large enough for the point-to-point xGMI
+rings).  Chunks go out in the same order on every rank.  ``chunks=1`` is one all-reduce
+of the whole buffer after backward.
 
 Averaging matches DDP's: every gradient is divided by the world size, then summed
 across ranks (exact for power-of-two world sizes), so both give the same bits.
@@ -35,12 +46,15 @@ class FlatGradAllReduce:
     reductions under torch.distributed.  Do not also wrap the same parameters in
     DistributedDataParallel: its hooks read gradients during backward."""
 
-    def __init__(self, params, group=None):
+    LEARN = 1   # group_blocks while the layout is learnt: every block reported on its own
+
+    def __init__(self, params, group=None, chunks=4):
         if not (dist.is_available() and dist.is_initialized()):
             raise RuntimeError("FlatGradAllReduce: torch.distributed is not initialized")
         self.params = [p for p in params if p.requires_grad]
         self.group = group
         self.world = dist.get_world_size(group)
+        self.chunks = max(1, int(chunks))
         with torch.no_grad():
             for bucket in self._buckets(self.params):
                 flat = _flatten_dense_tensors(bucket)
@@ -48,16 +62,41 @@ class FlatGradAllReduce:
                                group=group)
                 for p, v in zip(bucket, _unflatten_dense_tensors(flat, bucket)):
                     p.copy_(v)
-        # one persistent gradient buffer per (device, dtype); each parameter owns a view.
-        # The deferred TemporalBlock backwards write their gradients straight into it, so
-        # after a backward pass most gradients are already in place.
+        self._layout(self._buckets(self.params), None)
+        self._reported = []     # this step's hook reports (lists of parameters), in order
+        self._final = set()     # ids of parameters final in their views this step
+        self._launched = {}     # (arena, chunk) -> async all-reduce work
+        self._learnt = False
+        self.early_chunks = 0   # chunks all-reduced during a backward pass (overlapped)
+        self._hook_devs = []
+        self.group_blocks = self.LEARN
+        if self.chunks > 1:
+            for bucket in self._buckets(self.params):
+                if bucket[0].is_cuda and bucket[0].device not in self._hook_devs:
+                    ctn_ops.register_exchange_hook(bucket[0].device, self)
+                    self._hook_devs.append(bucket[0].device)
+
+    def close(self):
+        """Stop overlapping with the backward pass (unregister the ctn_ops hook)."""
+        for d in self._hook_devs:
+            ctn_ops.unregister_exchange_hook(d, self)
+        self._hook_devs = []
+
+    def _layout(self, buckets, bounds):
+        """One persistent gradient buffer per (device, dtype) bucket, in the bucket's
+        parameter order, each parameter owning a view; bounds[i] = the chunks of bucket i
+        as (first, end) parameter index ranges (None: one chunk)."""
         self._arenas = []
         views = {}
-        for bucket in self._buckets(self.params):
-            flat = torch.empty(sum(p.numel() for p in bucket), device=bucket[0].device, dtype=bucket[0].dtype)
-            vs = _unflatten_dense_tensors(flat, bucket)
-            self._arenas.append((bucket, flat, vs))
-            views.update({id(p): v for p, v in zip(bucket, vs)})
+        for i, g in enumerate(buckets):
+            flat = torch.empty(sum(p.numel() for p in g), device=g[0].device, dtype=g[0].dtype)
+            vs = _unflatten_dense_tensors(flat, g)
+            offs = [0]
+            for p in g:
+                offs.append(offs[-1] + p.numel())
+            chunks = bounds[i] if bounds is not None else [(0, len(g))]
+            self._arenas.append((g, flat, vs, [(a, b, offs[a], offs[b]) for a, b in chunks]))
+            views.update({id(p): v for p, v in zip(g, vs)})
         ctn_ops.register_synced_after_backward(self.params, [views[id(p)] for p in self.params])
 
     @staticmethod
@@ -67,6 +106,40 @@ class FlatGradAllReduce:
             by.setdefault((t.device, t.dtype), []).append(t)
         return list(by.values())
 
+    # ---- ctn_ops exchange hook (called from the backward pass, in block order)
+    def on_reduced(self, params):
+        """A group of deferred blocks' gradients is final, in place in their views: launch
+        every chunk, in order, whose parameters are all final."""
+        self._reported.append(list(params))
+        self._final.update(id(p) for p in params)
+        if self._learnt:
+            self._launch(final_only=True)
+
+    def _launch(self, final_only):
+        for ai, (g, flat, vs, chunks) in enumerate(self._arenas):
+            for ci, (a, b, o0, o1) in enumerate(chunks):
+                if (ai, ci) in self._launched:
+                    continue
+                if final_only and not all(id(p) in self._final for p in g[a:b]):
+                    return            # in order: every rank issues the same sequence
+                if not final_only:
+                    self._gather(g[a:b], vs[a:b])
+                part = flat[o0:o1]
+                part.div_(self.world)
+                self._launched[(ai, ci)] = dist.all_reduce(part, group=self.group, async_op=True)
+                self.early_chunks += final_only
+
+    @staticmethod
+    def _gather(params, views):
+        for p, v in zip(params, views):
+            g = p.grad
+            if g is v:               # written in place by a deferred block backward
+                continue
+            if g is None:
+                v.zero_()            # an unused parameter contributes zeros (as DDP)
+            else:                    # accumulated elsewhere (encoder, decoder, ...)
+                v.copy_(g)
+
     @torch.no_grad()
     def sync(self):
         """All-reduce (mean) every parameter gradient; a parameter without a gradient on
@@ -74,15 +147,38 @@ class FlatGradAllReduce:
         the mean.  Afterwards each ``p.grad`` is the parameter's view of the persistent
         buffer (as DDP's gradient_as_bucket_view makes them): keep a copy, not the tensor,
         to hold a gradient past the next step."""
-        for bucket, flat, views in self._arenas:
-            for p, v in zip(bucket, views):
-                g = p.grad
-                if g is v:               # written in place by a deferred block backward
-                    continue
-                if g is None:
-                    v.zero_()
-                else:                    # accumulated elsewhere (encoder, decoder, ...)
-                    v.copy_(g)
+        self._launch(final_only=False)
+        for w in self._launched.values():
+            w.wait()                 # the current stream waits for RCCL's
+        for g, flat, vs, _ in self._arenas:
+            for p, v in zip(g, vs):
                 p.grad = v
-            flat.div_(self.world)
-            dist.all_reduce(flat, group=self.group)
+        if not self._learnt and self._hook_devs:
+            self._learn()
+        self._reported, self._final, self._launched = [], set(), {}
+
+    def _learn(self):
+        """After the first step: the blocks the hook reported, in report order, in
+        `chunks - 1` groups of consecutive blocks, then every other parameter."""
+        blocks = [grp for grp in self._reported if grp]
+        self._learnt = True
+        if len(blocks) < 2:
+            self.group_blocks = 1 << 30   # nothing to overlap: one exchange after backward
+            return
+        per = -(-len(blocks) // (self.chunks - 1))
+        self.group_blocks = per
+        groups = [[p for grp in blocks[i:i + per] for p in grp] for i in range(0, len(blocks), per)]
+        seen = {id(p) for grp in groups for p in grp}
+        groups.append([p for p in self.params if id(p) not in seen])
+        buckets, bounds = {}, {}
+        for grp in groups:
+            firsts = {}
+            for p in grp:
+                key = (p.device, p.dtype)
+                lst = buckets.setdefault(key, [])
+                firsts.setdefault(key, len(lst))
+                lst.append(p)
+            for key, a in firsts.items():
+                bounds.setdefault(key, []).append((a, len(buckets[key])))
+        keys = list(buckets)
+        self._layout([buckets[k] for k in keys], [bounds[k] for k in keys])

@@ -174,6 +174,7 @@ _SIGS = {
     "ctn_timer_read_kind": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                            ctypes.POINTER(ctypes.c_int)]),
     "ctn_device_status": (ctypes.c_int, [c_void_p, ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]),
+    "ctn_tblock_plan": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_char_p, c_size_t]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)

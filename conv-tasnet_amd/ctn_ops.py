@@ -5,6 +5,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 import weakref
 from dataclasses import dataclass
 
@@ -224,20 +225,71 @@ def _grad_buffer(p):
 
 class _TaskState:
     """What one backward pass (device, autograd graph task) leaves for its end: the
-    contexts whose parameter uses it spent, and its deferred block backwards."""
-    __slots__ = ("tokens", "deferred")
+    contexts whose parameter uses it spent, and its deferred block backwards (entries
+    before `flushed` were already reduced for an exchange hook)."""
+    __slots__ = ("tokens", "deferred", "flushed")
 
     def __init__(self):
         self.tokens, self.deferred = [], []   # weak references: a dropped graph's tokens die
+        self.flushed = 0
+
+
+# Post-backward gradient exchanges that overlap the backward pass (ctn_dist.FlatGradAllReduce
+# with chunks > 1): device -> hook.  Every `hook.group_blocks` deferred block backwards the
+# pass reduces those blocks' gradients at once (instead of all at the pass's end) and calls
+# hook.on_reduced(params), so the exchange can all-reduce them while the rest of the
+# backward runs.
+_EXCHANGE_HOOKS = {}
+
+
+def register_exchange_hook(device, hook):
+    _EXCHANGE_HOOKS[torch.device(device)] = hook
+
+
+def unregister_exchange_hook(device, hook):
+    if _EXCHANGE_HOOKS.get(torch.device(device)) is hook:
+        del _EXCHANGE_HOOKS[torch.device(device)]
+
+
+def _reduce_entries(entries):
+    """One batched reduction (ctn_tblock_reduce_grads) of deferred block backwards."""
+    if not entries:
+        return
+    lib = L.load()
+    n = len(entries)
+    descs = (L.TBlockDesc * n)(*[e[0] for e in entries])
+    grads = (L.TBlockGrads * n)(*[e[1] for e in entries])
+    parts = (ctypes.c_void_p * n)(*[e[2].data_ptr() for e in entries])
+    L.check(lib.ctn_tblock_reduce_grads(descs, grads, parts, n, entries[0][4]), "ctn_tblock_reduce_grads")
 
 
 _TASKS = {}
+
+
+def _nested_backward() -> bool:
+    """This thread is running a backward pass from inside another one's node (a reentrant
+    torch.utils.checkpoint, a Function whose backward calls autograd): the outer pass's
+    torch.autograd backward entry is on this thread's Python stack.  A top-level pass runs
+    its nodes on the engine's device thread, whose stack holds no such frame."""
+    f = sys._getframe(1)
+    while f is not None:
+        if f.f_code.co_name in ("_engine_run_backward", "run_backward") and "autograd" in f.f_code.co_filename:
+            return True
+        f = f.f_back
+    return False
 
 
 def _task_state(dev) -> "_TaskState":
     key = (dev, torch._C._current_graph_task_id())
     st = _TASKS.get(key)
     if st is None:
+        # State of another pass on this device: the pass around this one (nested: keep it,
+        # it ends after this one) or a pass that raised before its end (top-level: drop it;
+        # its callback never ran).  The stack walk runs only in that rare case.
+        others = [k for k in _TASKS if k[0] == dev]
+        if others and not _nested_backward():
+            for k in others:
+                del _TASKS[k]
         st = _TASKS[key] = _TaskState()
         torch.autograd.Variable._execution_engine.queue_callback(lambda: _end_of_backward(key))
     return st
@@ -249,20 +301,13 @@ def _end_of_backward(key):
     the pass's parameter uses are spent (a graph kept alive by a returned loss must not
     count as a pending use in the next step; released here and not at each node, because
     an immediate node's gradient is accumulated only after the node returns)."""
+    # only this pass's own state: a nested pass ends before the pass around it, whose
+    # deferred blocks must survive it (stale state of a raised pass is dropped by the next
+    # top-level pass, _task_state)
     st = _TASKS.pop(key, None)
-    dev, task = key
-    for k in [k for k in _TASKS if k[0] == dev and k[1] < task]:
-        del _TASKS[k]          # left by a backward pass that raised before its end
     if st is None:
         return
-    entries = st.deferred
-    if entries:
-        lib = L.load()
-        n = len(entries)
-        descs = (L.TBlockDesc * n)(*[e[0] for e in entries])
-        grads = (L.TBlockGrads * n)(*[e[1] for e in entries])
-        parts = (ctypes.c_void_p * n)(*[e[2].data_ptr() for e in entries])
-        L.check(lib.ctn_tblock_reduce_grads(descs, grads, parts, n, entries[0][4]), "ctn_tblock_reduce_grads")
+    _reduce_entries(st.deferred[st.flushed:])
     for r in st.tokens:
         t = r()
         if t is not None:
@@ -413,8 +458,16 @@ class TBlockFn(torch.autograd.Function):
                 "ctn_tblock_backward_deferred")
         for p, g in zip(ctx.param_refs, grads):
             p.grad = g
-        # the partials, gradients and their descriptors stay alive until the pass's end
-        _task_state(dev).deferred.append((L.TBlockDesc(*ctx.desc), gstruct, part, grads, stream))
+        # the partials, gradients and their descriptors stay alive until they are reduced
+        st = _task_state(dev)
+        st.deferred.append((L.TBlockDesc(*ctx.desc), gstruct, part, grads, stream, ctx.param_refs))
+        hook = _EXCHANGE_HOOKS.get(dev)
+        if hook is not None and len(st.deferred) - st.flushed >= hook.group_blocks:
+            group = st.deferred[st.flushed:]
+            _reduce_entries(group)
+            st.deferred[st.flushed:] = [None] * len(group)   # partials: free once enqueued
+            st.flushed = len(st.deferred)
+            hook.on_reduced([p for e in group for p in e[5]])
         return (gx, None, None, None, None) + (None,) * 9
 
 

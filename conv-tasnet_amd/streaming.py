@@ -104,6 +104,10 @@ class StreamingSeparator:
                 n1a=a1, n1b=b1, wd=ds[0].weight.detach()[:, 0, :].float().contiguous(),
                 alpha2=ds[2].weight.detach().float().contiguous(), n2a=a2, n2b=b2, w2_t=_t1x1(ds[4])))
         self.B, self.H = self.blocks[0]["w1_t"].shape if self.blocks else (bott.weight.shape[0], 0)
+        # the ctn_stream_model holds pointers into this snapshot: rebuild it (the old
+        # tensors are freed; a cached struct would hand the library dangling pointers)
+        self._wver = getattr(self, "_wver", 0) + 1
+        self._mkey = None
 
     def reset(self):
         self.samples = None          # [M, s] pending input samples
@@ -135,7 +139,7 @@ class StreamingSeparator:
     def _model_struct(self):
         """ctn_stream_model for ctn_stream_call (ABI v7): pointers into the snapshot and
         the rings, rebuilt when either changes."""
-        key = (id(self.rings),)
+        key = (id(self.rings), self._wver)
         if getattr(self, "_mkey", None) != key:
             blocks = (L.StreamBlockParams * max(1, len(self.blocks)))()
             for i, (b, ring) in enumerate(zip(self.blocks, self.rings)):
@@ -165,6 +169,10 @@ class StreamingSeparator:
             sk = (M, K, dev)
             stg = self._stage.get(sk)
             if stg is None:
+                # bounded like the library's graph cache (8 argument sets): chunk sizes
+                # that keep changing must not grow device memory without limit
+                while len(self._stage) >= 8:
+                    self._stage.pop(next(iter(self._stage)))
                 ns = (K - 1) * self.stride + m.L
                 stg = self._stage[sk] = dict(inp=torch.empty(M, ns, device=dev),
                                              out=torch.empty(M, m.C, K * self.stride, device=dev),

@@ -378,6 +378,13 @@ int ctn_stream_call(const ctn_stream_desc* d, const ctn_stream_model* model, int
                     int64_t ld_samples, const float* tail_in, float* tail_out, float* out, void* ws,
                     size_t ws_bytes, void* stream);
 
+/* Kernel plan of one TemporalBlock launch (no device work): writes a NUL-terminated list
+ * "step=kernel,..." of the kernels ctn_tblock_forward (backward = 0) or the backward entries
+ * (backward = 1) would choose for d, e.g. "pairA=dual_ws,dw_bwd=wave,gx=ws_n1bwd,dW1=cols".
+ * Shapes outside a kernel's limits (tensors of 2^31 bytes or more for the persistent
+ * kernels' 32-bit offsets) fall back to the tiled kernels; this is how a caller sees it. */
+int ctn_tblock_plan(const ctn_tblock_desc* d, int backward, char* out, size_t cap);
+
 /* -------------------------------------------------------------------------
  * Opt-in kernel timer (bench.py roofline; the reference has no counterpart — its
  * solver prints epoch wall time only, src/solver.py:178-188): when enabled, every

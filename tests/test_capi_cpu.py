@@ -149,3 +149,26 @@ def test_device_code_has_no_packed_fp32(tmp_path):
         n_mfma += txt.count("v_mfma_")
     assert n_mfma > 0, "disassembly found no MFMA: the check itself is broken"
     assert n_pk == 0, f"{n_pk} packed-FP32 instructions in the device code"
+
+
+def _plan(lib, backward, **kw):
+    buf = ctypes.create_string_buffer(256)
+    assert lib.ctn_tblock_plan(ctypes.byref(_desc(**kw)), backward, buf, 256) == 0
+    return dict(kv.split("=") for kv in buf.value.decode().split(","))
+
+
+def test_tblock_plan_bench_shape_and_2gb_fallback(lib):
+    """The persistent kernels (weight-stationary GEMMs, wave-specialised dual GEMM,
+    wave-item depthwise kernels) address their tiles with 32-bit offsets: at 2^21 frame
+    rows (M*Kp*512*2 bytes = 2 GiB) the launch must fall back to the tiled kernels
+    (ADVICE r04), while the bench shape takes the persistent ones."""
+    fwd, bwd = _plan(lib, 0, M=32), _plan(lib, 1, M=32)
+    assert fwd == {"gemm1": "ws", "dw_fwd": "wave", "gemm2": "ws"}, fwd
+    assert bwd["pairA"] == "dual_ws" and bwd["dw_bwd"] == "wave" and bwd["gx"] == "ws_n1bwd", bwd
+    big = dict(M=656, K=3199, Kp=3200)        # 656 * 3200 = 2,099,200 rows >= 2^21
+    fwd, bwd = _plan(lib, 0, **big), _plan(lib, 1, **big)
+    assert fwd == {"gemm1": "rows", "dw_fwd": "lane", "gemm2": "rows"}, fwd
+    assert bwd["pairA"] not in ("dual_ws", "dual", "ws+cols") and bwd["dw_bwd"] == "lane", bwd
+    assert "gx" not in bwd or bwd["gx"] != "ws_n1bwd", bwd
+    just_below = dict(M=655, K=3199, Kp=3200)  # 2,096,000 rows
+    assert _plan(lib, 1, **just_below)["pairA"] == "dual_ws"

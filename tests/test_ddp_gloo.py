@@ -126,7 +126,9 @@ def _flat_worker(rank, world, port, q):
         a.grad = torch.full((4,), float(rank + 1 + step))
         b.grad = None if rank == 1 else torch.full((2, 3), 3.0 * rank)   # unused on rank 1
         sync.sync()
-        q.put((rank, step, a.detach().clone(), a.grad.clone(), b.grad.clone()))
+        # numpy, not tensors: a tensor travels as a shared-memory handle that vanishes if
+        # this process exits before the parent unpickles it
+        q.put((rank, step, a.detach().numpy().copy(), a.grad.numpy().copy(), b.grad.numpy().copy()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -147,6 +149,7 @@ def test_flat_exchange_mean_unused_and_reuse():
         p.join(timeout=60)
         assert p.exitcode == 0
     for rank, step, a, ga, gb in res:
+        a, ga, gb = torch.from_numpy(a), torch.from_numpy(ga), torch.from_numpy(gb)
         assert torch.equal(a, torch.zeros(4))
         torch.testing.assert_close(ga, torch.full((4,), (1 + 2 + 3) / 3 + step))
         torch.testing.assert_close(gb, torch.full((2, 3), (0.0 + 0.0 + 6.0) / 3))

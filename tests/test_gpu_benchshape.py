@@ -214,7 +214,10 @@ def test_model_c5_shape_bf16_vs_oracle():
     """c5's per-GPU dispatch in bf16 (3 speakers, N=512, 8 s @ 8 kHz: K=6399 frames,
     a 1536-channel mask) at its per-GPU batch of 16 utterances (BASELINE.json
     configs[4]: global 128 over 8 GPUs): per-utterance SI-SNR within 0.1 dB of the
-    fp32 oracle, estimates within 5e-2, weight-gradient norms within 10 %."""
+    fp32 oracle, estimates within 5e-2, and every weight / norm-affine gradient TENSOR
+    within 0.25 relative L2 of the oracle's (a permuted or misplaced gradient of equal
+    norm must fail; 0.25 is the random-weight bf16 bound of the c4 test below: bf16
+    storage through 32 residual blocks moves the deep blocks' gradients by 0.1-0.2)."""
     import pit_criterion as pc
     import synthetic
     cfg_d = dict(PAPER, N=512, C=3)
@@ -235,11 +238,14 @@ def test_model_c5_shape_bf16_vs_oracle():
     for b in range(M):
         assert rel(est_m[b].detach().cpu(), est_r[b]) < 5e-2, b
     pg = dict(model.named_parameters())
+    errs = {}
     for n, shape in O.param_shapes(cfg):
-        if len(shape) < 2:
-            continue
-        g, gr = pg[n].grad.detach().cpu(), grads_r[n]
-        assert abs(float(g.norm()) / float(gr.norm()) - 1) < 0.1, n
+        if shape == (1,):
+            continue   # PReLU alpha in bf16: cancellation-heavy scalar (see test_gpu_tblock.py)
+        g, gr = pg[n].grad.detach().cpu().reshape(grads_r[n].shape), grads_r[n]
+        errs[n] = rel(g, gr)
+        assert errs[n] < 0.25, (n, errs[n])
+    print("c5 worst per-tensor gradient errors", sorted(errs.items(), key=lambda kv: -kv[1])[:4])
 
 
 def _load(name):

@@ -10,8 +10,10 @@ src/train.py:120-122's DataParallel).  Checked against the single-process
 full-batch HIP step: averaged gradients equal the full-batch gradients (loss =
 batch mean, equal shards), and both ranks end with identical parameters.
 fp32 (tight) and bf16 with packed weights (the throughput mode).  The same with the
-bench's default exchange, ctn_dist.FlatGradAllReduce (one all-reduce after backward,
-the TemporalBlock gradient reductions deferred to the end of the pass).  GPU only.
+bench's default exchange, ctn_dist.FlatGradAllReduce (the TemporalBlock gradient
+reductions deferred and run in groups during the backward pass, each group's slice of
+the persistent buffer all-reduced while the backward goes on, the rest after it).
+GPU only.
 """
 import os
 import socket
@@ -97,6 +99,8 @@ def _worker(rank, world, port, bf16, view, q):
         loss, grads, params = _step(net, mix[shard].to(dev), src[shard].to(dev), bf16, sync)
         # deferral under torch.distributed only for the post-backward exchange
         assert (ctn_ops.DEFERRED_BLOCKS > n0) == (view == "flat"), ctn_ops.DEFERRED_BLOCKS - n0
+        if sync is not None:   # chunked exchange: the early chunks went out during backward
+            assert sync.early_chunks >= 2, sync.early_chunks
         q.put((rank, loss, [g.numpy() for g in grads], [p.numpy() for p in params]))
         dist.barrier()
     finally:

@@ -182,3 +182,40 @@ def test_deferred_with_previous_graph_alive():
         assert ctn_ops.DEFERRED_BLOCKS - n0 == 6
         for a, p in zip(ref, m.parameters()):
             assert torch.equal(a, p.grad)
+
+
+def test_deferred_with_reentrant_checkpoint():
+    """A reentrant torch.utils.checkpoint around the first TemporalBlock of a chain (ADVICE
+    r04): its recomputation and backward run as a nested backward pass inside the outer
+    one, after the outer pass has deferred the later blocks.  The nested pass must not drop
+    the outer pass's deferred state (the outer blocks' gradients would never be reduced),
+    and every gradient equals the chain's without deferral."""
+    import ctn_ops
+    import conv_tasnet as ct
+    from torch.utils.checkpoint import checkpoint
+    import ctn_lib as L
+    torch.manual_seed(6)
+    tcn = ct.TemporalConvNet(64, 64, 128, 3, 3, 2, 2, norm_type="gLN").to(DEV)
+    blocks = list(tcn.blocks())
+    fr = ctn_ops.Frames.of(2, 1000)
+    x0 = torch.randn(2, 64, 1000, device=DEV)
+
+    def run(defer):
+        for p in tcn.parameters():
+            p.grad = None
+        x = ctn_ops.ncw_to_rows(x0, fr, torch.bfloat16).requires_grad_(True)
+        r = checkpoint(lambda t: blocks[0]._forward_rows(t, fr, L.NORM_GLN, None, False, defer), x,
+                       use_reentrant=True)
+        for b in blocks[1:]:
+            r = b._forward_rows(r, fr, L.NORM_GLN, None, False, defer)
+        (ctn_ops.rows_to_ncw(r, fr, torch.float32) ** 2).sum().backward()
+        return [p.grad.detach().clone() for b in blocks for p in b.parameters()], x.grad.clone()
+
+    ref, gref = run(False)
+    n0 = ctn_ops.DEFERRED_BLOCKS
+    got, g = run(True)
+    assert ctn_ops.DEFERRED_BLOCKS > n0
+    assert torch.equal(g, gref)
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b)
+    assert not ctn_ops._TASKS

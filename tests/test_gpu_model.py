@@ -167,20 +167,25 @@ def test_bn_running_statistics_and_eval_mode():
 
 
 def test_bn_bf16_training_step():
-    """bf16 activations through the BN path: the estimate stays within 5e-2 relative
-    L2 of the fp32 reference and every gradient is finite with the reference norm
-    to 10 % (the bf16 bar of test_model_bf16_sisnri_within_0p1db)."""
+    """bf16 activations through the BN path against the REFERENCE's gradients
+    (model_bn.npz, BatchNorm1d in training mode): the estimate within 5e-2 relative L2,
+    and every parameter gradient tensor (not only its norm: a permuted or misplaced
+    gradient of equal norm must fail) within 0.1 relative L2 per tensor, PReLU alphas
+    (cancellation-heavy scalars in bf16) within 0.25 relative."""
     g = load("model_bn.npz")
     cfg = cfg_of(g)
     model = build(cfg, g)
     est, loss, max_snr, reord = run(model, g, bf16=True)
     assert rel(est.detach().cpu().numpy(), g["est"]) < 5e-2
     params = dict(model.named_parameters())
+    worst = {}
     for n, shape in O.param_shapes(cfg):
         gr = params[n].grad.detach().cpu().reshape(-1).numpy()
+        ref = g["g:" + n].reshape(-1)
         assert np.isfinite(gr).all(), n
-        if len(shape) >= 2:
-            assert abs(np.linalg.norm(gr) / float(g["gnorm:" + n]) - 1) < 0.1, n
+        worst[n] = e = rel(gr, ref)
+        assert e < (0.25 if shape == (1,) else 0.1), (n, e)
+    print("worst per-tensor gradient errors", sorted(worst.items(), key=lambda kv: -kv[1])[:4])
 
 
 @pytest.mark.parametrize("L_", [20, 16])

@@ -173,3 +173,43 @@ def test_stream_graph_replay_matches_direct_launches(monkeypatch):
             parts.append(s.flush())
         outs.append(torch.cat(parts, dim=2))
     assert torch.equal(outs[0], outs[1])
+
+
+def test_stream_refresh_weights_mid_stream():
+    """refresh_weights() in the middle of a stream (the one-call path cached its
+    model struct by the rings only and then replayed a graph over freed weight copies):
+    after the refresh the one-call streamer must equal the per-stage entries (which rebuild
+    their pointers on every call) running the same pushes and the same refresh."""
+    import streaming
+    mix = torch.randn(2, 3000, device=DEV)
+    outs = []
+    for one in (True, False):
+        m = _model(seed=5)
+        s = streaming.StreamingSeparator(m, max_frames=8)
+        s.one_call = one
+        parts = [s.push(mix[:, i:i + 320]) for i in range(0, 1600, 320)]
+        with torch.no_grad():
+            for p in m.parameters():
+                p.mul_(0.9)
+        s.refresh_weights()
+        torch.cuda.empty_cache()   # the old snapshot's memory goes back to the device pool
+        junk = [torch.randn(1 << 20, device=DEV) for _ in range(4)]   # and gets reused
+        parts += [s.push(mix[:, i:i + 320]) for i in range(1600, 3000, 320)]
+        parts.append(s.flush())
+        del junk
+        outs.append(torch.cat(parts, dim=2))
+    assert rel(outs[0], outs[1]) < 1e-5, rel(outs[0], outs[1])
+
+
+def test_stream_staging_is_bounded():
+    """Pushes of many different lengths keep at most 8 staging buffer sets (the library's
+    graph cache holds 8 argument sets)."""
+    import streaming
+    m = _model()
+    s = streaming.StreamingSeparator(m, max_frames=64)
+    mix = torch.randn(1, 20000, device=DEV)
+    i = 0
+    for n in range(40, 800, 40):
+        s.push(mix[:, i:i + n])
+        i += n
+    assert len(s._stage) <= 8

@@ -161,3 +161,42 @@ def test_adam_plan_reused_across_steps():
             a.grad.copy_(g) if a.grad is not None else setattr(a, "grad", g)
         o.step()
     assert len(o._plans) == 1
+
+
+@pytest.mark.gpu
+def test_fast_paths_match_torch():
+    """The host fast paths (same parameters, gradient pointers and sizes as the previous
+    fully checked call: ctn_optim._clip_fast, Adam._fast_step) against torch's clip + Adam
+    over steps with in-place gradients, then a step where one parameter has no gradient
+    (full path again), then the state_dict step counts."""
+    import ctn_optim
+    dev = torch.device("cuda")
+    ps = [torch.nn.Parameter(t) for t in _params(dev)]
+    qs = [torch.nn.Parameter(t.clone()) for t in _params(dev)]
+    o_hip = ctn_optim.Adam(ps, lr=1e-3)
+    o_ref = torch.optim.Adam(qs, lr=1e-3, foreach=False)
+    for a, b in zip(ps, qs):
+        a.grad, b.grad = torch.zeros_like(a), torch.zeros_like(b)
+    fast_steps = 0
+    for step in range(6):
+        for a, b, g in zip(ps, qs, _grads(ps, 40 + step)):
+            a.grad.copy_(g)
+            b.grad.copy_(g)
+        n_hip = ctn_optim.clip_grad_norm_(ps, 1.0)
+        n_ref = torch.nn.utils.clip_grad_norm_(qs, 1.0)
+        torch.testing.assert_close(n_hip, n_ref, rtol=1e-6, atol=0)
+        o_hip.step()
+        o_ref.step()
+        fast_steps += bool(o_hip._fast.get(0) and o_hip._fast[0][4])
+    assert fast_steps >= 4
+    ps[1].grad, qs[1].grad = None, None
+    for a, b, g in zip(ps, qs, _grads(ps, 60)):
+        if a.grad is not None:
+            a.grad.copy_(g)
+            b.grad.copy_(g)
+    o_hip.step()
+    o_ref.step()
+    for a, b in zip(ps, qs):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+    sd = o_hip.state_dict()
+    assert [float(sd["state"][i]["step"]) for i in range(3)] == [7.0, 6.0, 7.0]

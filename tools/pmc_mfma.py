@@ -9,10 +9,14 @@ import csv, glob, os, sys
 from collections import defaultdict
 root = sys.argv[1]
 json_out = sys.argv[2] if len(sys.argv) > 2 else None
-KINDS = {   # bench.py timer kinds -> kernel name (bf16 throughput mode)
+KINDS = {   # bench.py timer kinds (include/ctn.h CTN_TIMER_*) -> kernel name (bf16, gLN c2 shape)
     "1": "gemm_ws_kernel<0, 0, 1, 2, 8, 16, 2, 1>",
-    "2": "dw_fwd_kernel<unsigned short, 0, 3, false>",
-    "3": "gemm_dual_ws_kernel<0, 6, 5, false>",   # the wave-specialised pair-A dual
+    "2": "dw_fwd_wave_kernel<0, false>",
+    "3": "gemm_dual_ws_kernel<0, ",   # the wave-specialised pair-A dual (gLN)
+    "4": "dw_bwd_wave_kernel<0, false>",
+    "5": "gemm_ws_kernel<3, 0, 2, 2, 16, 8, 1, 1>",
+    "6": "gemm_cols_kernel<unsigned short, 0, 0, 0>",
+    "7": "gemm_ws_kernel<2, 0, 2, 2, 16, 8, 1, 1>",
 }
 vals = defaultdict(lambda: defaultdict(list))
 for f in sorted(glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)):

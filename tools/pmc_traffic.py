@@ -15,10 +15,14 @@ import os
 import sys
 from collections import defaultdict
 
-KINDS = {   # bench.py timer kinds -> kernel name (bf16 throughput mode)
+KINDS = {   # bench.py timer kinds (include/ctn.h CTN_TIMER_*) -> kernel name (bf16, gLN c2 shape)
     "1": "ctn::gemm_ws_kernel<0, 0, 1, 2, 8, 16, 2, 1>",
-    "2": "ctn::dw_fwd_kernel<unsigned short, 0, 3, false>",
+    "2": "dw_fwd_wave_kernel<0, false>",
     "3": "gemm_dual_ws_kernel<0, ",   # the wave-specialised pair-A dual (gLN)
+    "4": "dw_bwd_wave_kernel<0, false>",
+    "5": "ctn::gemm_ws_kernel<3, 0, 2, 2, 16, 8, 1, 1>",
+    "6": "ctn::gemm_cols_kernel<unsigned short, 0, 0, 0>",
+    "7": "ctn::gemm_ws_kernel<2, 0, 2, 2, 16, 8, 1, 1>",
 }
 
 
