@@ -62,7 +62,7 @@ build/dual_bench_%: tools/microbench/dual_bench.hip $(PKG)/csrc/ctn_gemm_dual.hi
 .PHONY: dualbench
 
 # wave-specialised pair-A dual GEMM vs gemm_dual_kernel: build/dual_ws_bench_<bits>
-DV_EXPS := 0 1 2 4 6
+DV_EXPS := 0 1 2 4 8 32 34 64 96
 dualws: $(patsubst %,build/dual_ws_bench_%,$(DV_EXPS))
 build/dual_ws_bench_%: tools/microbench/dual_ws_bench.hip $(PKG)/csrc/ctn_dual_ws.hip $(PKG)/csrc/ctn_gemm_dual.hip $(HDR)
 	@mkdir -p build
@@ -87,6 +87,16 @@ build/dual_ws_var_%: tools/microbench/dual_ws_bench.hip $(PKG)/csrc/ctn_dual_ws.
 	  -DCTN_DV_NSL=$(word 2,$(subst _, ,$*)) -DCTN_DV_CJ=$(word 3,$(subst _, ,$*)) -DCTN_DV_EXP=$(word 4,$(subst _, ,$*)) $< -o $@
 
 .PHONY: dualwsvar
+
+# N-image variants: build/dual_ws_nv_<nimg>_<nc>_<cjn>_<exp> (CTN_DV_NIMG, CTN_DV_NC, CTN_DV_CJN, CTN_DV_EXP)
+NV_VARS := 0_8_4_0 1_8_4_0 1_8_2_0 1_4_4_0 1_4_2_0
+dualwsnv: $(patsubst %,build/dual_ws_nv_%,$(NV_VARS))
+build/dual_ws_nv_%: tools/microbench/dual_ws_bench.hip $(PKG)/csrc/ctn_dual_ws.hip $(PKG)/csrc/ctn_gemm_dual.hip $(HDR)
+	@mkdir -p build
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -Iinclude $(DEVFLAGS) -DCTN_DV_NIMG=$(word 1,$(subst _, ,$*)) \
+	  -DCTN_DV_NC=$(word 2,$(subst _, ,$*)) -DCTN_DV_CJN=$(word 3,$(subst _, ,$*)) -DCTN_DV_EXP=$(word 4,$(subst _, ,$*)) $< -o $@
+
+.PHONY: dualwsnv
 .PHONY: dualwsdbg
 
 # library variants for A/B runs (tools/gpu_variants.sh, loaded through CTN_HIP_LIB):

@@ -354,8 +354,9 @@ def main():
     # parameter-gradient reductions of all blocks batched at the end of backward (on by
     # default; CTN_DEFER_REDUCE=0 for A/B against the per-block reductions)
     model.defer_grad_reduce = os.environ.get("CTN_DEFER_REDUCE", "1") == "1"
-    # gradient exchange across ranks: "flat" (default) = one all-reduce of all gradients
-    # after backward (ctn_dist.FlatGradAllReduce; the deferred reductions stay on),
+    # gradient exchange across ranks: "flat" (default) = all-reduces of a persistent flat
+    # gradient buffer, CTN_FLAT_CHUNKS - 1 of them during backward as groups of deferred
+    # block reductions finish, the rest after it (ctn_dist.FlatGradAllReduce),
     # "ddp" = DistributedDataParallel's bucket hooks during backward (per-block reductions)
     sync_kind = os.environ.get("CTN_GRAD_SYNC", "flat")
     if sync_kind not in ("flat", "ddp"):
@@ -363,7 +364,8 @@ def main():
     grad_sync = None
     if use_ddp and sync_kind == "flat":
         import ctn_dist
-        grad_sync = ctn_dist.FlatGradAllReduce(model.parameters())
+        grad_sync = ctn_dist.FlatGradAllReduce(model.parameters(),
+                                               chunks=int(os.environ.get("CTN_FLAT_CHUNKS", "4")))
     elif use_ddp:
         # gradients as views into the RCCL buckets (no per-step copy into the buckets),
         # one fixed graph (the reducer skips its unused-parameter search each step)

@@ -41,7 +41,13 @@ typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 constexpr int DV_TM = 32;                        // frame rows per tile
-constexpr int DV_NR = 4, DV_NC = 8, DV_NMW = 4;  // row / column / memory waves
+// column waves: 8 (64 dW2 accumulators each, 4 waves per SIMD, 128 VGPRs per wave) or 4
+// (128 accumulators each, 3 waves per SIMD, 168 VGPRs per wave)
+#ifndef CTN_DV_NC
+#define CTN_DV_NC 8
+#endif
+constexpr int DV_NR = 4, DV_NC = CTN_DV_NC, DV_NMW = 4;  // row / column / memory waves
+static_assert(DV_NC == 4 || DV_NC == 8, "column waves");
 constexpr int DV_ND = DV_NR + DV_NC;             // waves that publish DONE
 constexpr int DV_NT = (DV_ND + DV_NMW) * 64;     // 1024 threads
 constexpr int DV_KB = 8, DV_KR = 256;            // reduction of the row part (gy channels)
@@ -84,6 +90,23 @@ static_assert(DV_PF_CLN >= 1 && DV_PF_CLN <= DV_NSL - 1, "ring look-ahead (cLN)"
 #endif
 constexpr int DV_CJ = CTN_DV_CJ, DV_CI = 16 / DV_CJ;
 static_assert(DV_CJ == 1 || DV_CJ == 2 || DV_CJ == 4, "column blocks per column wave");
+// N image (CTN_DV_NIMG=1, default; RAWB=1 only): the row waves, which already apply PReLU +
+// norm to the raw d of their 16-byte granules in the epilogue, also write op(d) =
+// gamma2 * hat a2 + beta2 (bf16) over that raw d in the B image, and the column waves wait
+// for the four row waves' DONE of the tile instead of FULL and read op(d) fragments without
+// any transform: op(d) is computed once per element instead of twice, the column waves lose
+// their transform chain and the B statistics, and their split is free to read the fewest
+// fragments (CTN_DV_CJN column blocks per wave).  op(d) is rounded from fmaf(hat a, gamma,
+// beta) instead of fmaf(a - mean, rstd * gamma, beta): dW2 differs from the NIMG=0 kernel
+// in the last bits of some bf16 operands; C and the statistics are unchanged.
+#ifndef CTN_DV_NIMG
+#define CTN_DV_NIMG 0
+#endif
+constexpr bool DV_NI = CTN_DV_NIMG && CTN_DV_RAWB;
+#ifndef CTN_DV_CJN
+#define CTN_DV_CJN 4
+#endif
+static_assert(CTN_DV_CJN == 1 || CTN_DV_CJN == 2 || CTN_DV_CJN == 4 || CTN_DV_CJN == 8, "column blocks per column wave (NIMG)");
 // COLS mode (no operand transform to share): the split that reads the fewest fragments
 #ifndef CTN_DV_CJC
 #define CTN_DV_CJC 4
@@ -99,7 +122,9 @@ constexpr int DV_LA = CTN_DV_LA;
 
 // Bound-finding builds only (tools/microbench/dual_ws_bench.hip -DCTN_DV_EXP=<bits>):
 // bit 0 consumers skip all arithmetic (wait FULL, publish DONE), bit 1 no column part,
-// bit 2 no epilogue math, bit 3 no C stores, bit 4 row waves store zeros and nothing else.
+// bit 2 no epilogue math, bit 3 no C stores, bit 4 row waves store zeros and nothing else,
+// bit 5 the memory waves issue no DMA (consumers read whatever the ring holds), bit 6 the
+// row waves skip all arithmetic.
 #ifndef CTN_DV_EXP
 #define CTN_DV_EXP 0
 #endif
@@ -219,7 +244,9 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
   __shared__ __attribute__((aligned(16))) uint32_t fl_done[NSL][ND];   // per row / column wave
   __shared__ __attribute__((aligned(16))) float sgb[2][NS];            // gamma2 / beta2 of the slice
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // wave id through readfirstlane: wave-uniform to the compiler, so per-role pointers and
+  // offsets live in SGPRs (the row waves are at the 128-VGPR limit of 4 waves per SIMD)
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lr = lane & 15, lg = lane >> 4;
   const int S = p.Nout / NS;
   const int nr = (int)gridDim.x / S;   // row ranges
@@ -281,9 +308,14 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
     }
     const int cl = 32 * r + 8 * lg;
     bf16raw* Cg = reinterpret_cast<bf16raw*>(p.C);
-    float gam[8];
-    *reinterpret_cast<float4*>(gam) = *reinterpret_cast<const float4*>(p.gamma + n0 + cl);
-    *reinterpret_cast<float4*>(gam + 4) = *reinterpret_cast<const float4*>(p.gamma + n0 + cl + 4);
+    // gamma2 (and, NIMG, beta2) of the lane's 8 channels: registers, or (NIMG, where the
+    // registers are short) read per tile from the slice's LDS copy (p.bop.gamma == p.gamma:
+    // gemm_dual_ws_eligible)
+    float gamr[8];
+    if constexpr (!DV_NI) {
+      *reinterpret_cast<float4*>(gamr) = *reinterpret_cast<const float4*>(p.gamma + n0 + cl);
+      *reinterpret_cast<float4*>(gamr + 4) = *reinterpret_cast<const float4*>(p.gamma + n0 + cl + 4);
+    }
     const int rbase = lg * 256 + ((lr ^ ((lg & 1) * 12)) << 4);   // + rb * KB * 1024 + kb * 1024
     const int ro = DV_RB ? OFF_B + dv_rbgr(lr, 4 * r + lg)          // row lr; row 16 + lr at + 4096
                          : OFF_R + dv_roff(lr, 4 * r + lg);
@@ -306,7 +338,7 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
         if constexpr (CTN_DV_EXP & 16) {   // C stores only (zeros)
 #pragma unroll
           for (int rb = 0; rb < 2; ++rb) stg16(Cg + ((size_t)t * TM + 16 * rb + lr) * p.ldc + n0 + cl, v4u{0u, 0u, 0u, 0u});
-        } else if constexpr (!(CTN_DV_EXP & 1)) {
+        } else if constexpr (!(CTN_DV_EXP & 65)) {
           f32x4_t acc[2][2];
 #pragma unroll
           for (int rb = 0; rb < 2; ++rb)
@@ -348,6 +380,19 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
           // (Summing ga * a and scaling by rstd once per row saves one FMA per element but
           // cancels when |mean| >> the spread of a: not used.)
           float s1[2] = {0.f, 0.f}, q1[2] = {0.f, 0.f};
+          float gam[8], bet[8];
+          if constexpr (DV_NI) {
+            int co = cl >> 2;
+            asm volatile("" : "+v"(co));   // re-read per tile: hoisted, they would hold 16 VGPRs
+            const float4* g4 = reinterpret_cast<const float4*>(&sgb[0][0]);
+            *reinterpret_cast<float4*>(gam) = g4[co];
+            *reinterpret_cast<float4*>(gam + 4) = g4[co + 1];
+            *reinterpret_cast<float4*>(bet) = g4[NS / 4 + co];
+            *reinterpret_cast<float4*>(bet + 4) = g4[NS / 4 + co + 1];
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) gam[e] = gamr[e], bet[e] = 0.f;
+          }
 #pragma unroll
           for (int rb = 0; rb < 2; ++rb) {
             const v4u rw = *reinterpret_cast<const v4u*>(base + ro + rb * 4096);
@@ -360,6 +405,7 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
             float f[8];
             unpack_bf16x8(rw, f);
             if constexpr (!(CTN_DV_EXP & 4)) {
+              float nv[8];
 #pragma unroll
               for (int e = 0; e < 8; ++e) {
                 const float a = dv_prelu<LE1>(f[e], eal);
@@ -367,13 +413,18 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
                 const float ga = acc[rb][e >> 2][e & 3] * gam[e];
                 s1[rb] += ga;
                 q1[rb] = fmaf(ga, ah, q1[rb]);
+                if constexpr (DV_NI) nv[e] = ok ? fmaf(ah, gam[e], bet[e]) : 0.f;   // op(d); padded cLN frames 0
               }
+              if constexpr (DV_NI)   // over this lane's own raw granule (read above, by this wave only)
+                *reinterpret_cast<v4u*>(base + ro + rb * 4096) =
+                    v4u{pk_bf16(nv[0], nv[1]), pk_bf16(nv[2], nv[3]), pk_bf16(nv[4], nv[5]), pk_bf16(nv[6], nv[7])};
             }
             const v4u cv = {pk_bf16(acc[rb][0][0], acc[rb][0][1]), pk_bf16(acc[rb][0][2], acc[rb][0][3]),
                             pk_bf16(acc[rb][1][0], acc[rb][1][1]), pk_bf16(acc[rb][1][2], acc[rb][1][3])};
             // whole 16-byte lanes straight to memory (a wave covers 16 rows x 64 B)
             if constexpr (!(CTN_DV_EXP & 8))
-              stg16(Cg + ((size_t)t * TM + 16 * rb + lr) * p.ldc + n0 + cl, (CTN_DV_DBG & 16) ? rw : cv);
+              // wave-uniform 64-bit tile base + 32-bit lane offset (SGPR base, one VGPR)
+              stg16(Cg + (size_t)t * TM * p.ldc + n0 + (uint32_t)((16 * rb + lr) * p.ldc + cl), (CTN_DV_DBG & 16) ? rw : cv);
           }
           if constexpr (NK == NORM_GLN) {
             const int m = t / tpu;
@@ -413,7 +464,10 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
     // ======================= column waves =======================
     // wave c = (wp, wn) owns dW2 blocks p in [16 CI wp, +16 CI), n in [n0 + 16 CJ wn, +16 CJ):
     // dW2 += gy_tile^T . op(d)_tile, the reduction over the tile's 32 frame rows
-    constexpr int CJ = COLS ? DV_CJC : DV_CJ, CI = 16 / CJ;
+    // the slice's 16 x 8 blocks of 16 x 16: waves in a (NC / (8 / CJ)) x (8 / CJ) grid,
+    // each CI x CJ blocks
+    constexpr int CJ = COLS ? DV_CJC : (DV_NI ? CTN_DV_CJN : DV_CJ), CI = 16 * (8 / CJ) / DV_NC;
+    static_assert(CI >= 2 && CI <= 16 && CI % 2 == 0, "column split");
     const int c = wid - NR, wp = c / (8 / CJ), wn = c % (8 / CJ);
     f32x4_t dacc[CI][CJ];
 #pragma unroll
@@ -446,7 +500,8 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
       int slot = 0;
       uint32_t gen = 1;
       for (int t = t0; t < t1; ++t) {
-        dv_wait<4>(fl_full[slot], gen, p.err);
+        // NIMG: the row waves' DONE of the tile (they waited for FULL and wrote op(d))
+        dv_wait<4>((DV_NI && !COLS) ? fl_done[slot] : fl_full[slot], gen, p.err);
         const char* base = smem + slot * SLOT;
         if constexpr (!(CTN_DV_EXP & 3)) {
           const char* a = base + OFF_A;
@@ -458,7 +513,7 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
             const s16x4_t hi = dv_tr(bb + (DV_RB ? bbase[1] ^ (j << 5) : bbase[1] + j * DV_BST));
             bfr[j] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
           }
-          if constexpr (DV_RB && !COLS) {
+          if constexpr (DV_RB && !COLS && !DV_NI) {
             float mu[8], rs[8];
             if constexpr (NK == NORM_GLN) {
               const float2 st = *reinterpret_cast<const float2*>(base + OFF_ST);
@@ -583,6 +638,7 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
   // DMA instructions per wave and tile: 7 (st_wave), else 6 (RAWB=1 waves 1..3)
 
   auto dma = [&](int t) __attribute__((always_inline)) {
+    if constexpr (CTN_DV_EXP & 32) return;
     char* base = smem + ((t - t0) % NSL) * SLOT;
     const int tk = (t * TM) % Kp;
 #pragma unroll
@@ -684,6 +740,7 @@ bool gemm_dual_ws_eligible(const GemmDual& p) {
   if (!(p.Kred == DV_KR && p.Nout % DV_NS == 0 && p.epi == EPI_NORM_BWD && p.bop.kind == OP_PRELU_NORM)) return false;
   if (p.norm != NORM_GLN && p.norm != NORM_CLN) return false;
   if (p.bop.norm != p.norm || p.stats != p.bop.stats || p.bop.fold.slab) return false;
+  if (DV_NI && p.gamma != p.bop.gamma) return false;   // the row waves' gamma serves op(d)
   if (p.g.Kp % DV_TM || p.lda % 8 || p.ldb % 8 || p.ldc % 8 || p.ldw % 8) return false;
   if (p.g.rows() / DV_TM < 1) return false;
   // 32-bit tile offsets and buffer sizes (du_rsrc clamps at 2^31 bytes): larger tensors

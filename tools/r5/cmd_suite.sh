@@ -4,7 +4,7 @@ cd $GRAFT_REPO_ROOT
 O=gpurun_out/${1:-r5suite}
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 600 --timeout-method thread > $O/tests.log 2>&1; rc=$?
+timeout -k 10 900 python -u -m pytest ${TESTS:-tests} --maxfail=5 -v -m gpu --timeout 600 --timeout-method thread > $O/tests.log 2>&1; rc=$?
 tail -1 $O/tests.log
 grep -E "FAILED|Error" $O/tests.log | head -20
 [ $rc -eq 0 ] || exit $rc
