@@ -88,13 +88,15 @@ build/dual_ws_var_%: tools/microbench/dual_ws_bench.hip $(PKG)/csrc/ctn_dual_ws.
 
 .PHONY: dualwsvar
 
-# N-image variants: build/dual_ws_nv_<nimg>_<nc>_<cjn>_<exp> (CTN_DV_NIMG, CTN_DV_NC, CTN_DV_CJN, CTN_DV_EXP)
-NV_VARS := 0_8_4_0 1_8_4_0 1_8_2_0 1_4_4_0 1_4_2_0
+# N-image / column-wave variants: build/dual_ws_nv_<nimg>_<nc>_<cj>_<exp>_<la>
+# (CTN_DV_NIMG, CTN_DV_NC, CTN_DV_CJ = CTN_DV_CJN, CTN_DV_EXP, CTN_DV_LA)
+NV_VARS := 0_8_1_0_1 0_4_2_0_1 0_4_2_0_2 0_4_4_0_1 1_4_2_0_2
 dualwsnv: $(patsubst %,build/dual_ws_nv_%,$(NV_VARS))
 build/dual_ws_nv_%: tools/microbench/dual_ws_bench.hip $(PKG)/csrc/ctn_dual_ws.hip $(PKG)/csrc/ctn_gemm_dual.hip $(HDR)
 	@mkdir -p build
 	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -Iinclude $(DEVFLAGS) -DCTN_DV_NIMG=$(word 1,$(subst _, ,$*)) \
-	  -DCTN_DV_NC=$(word 2,$(subst _, ,$*)) -DCTN_DV_CJN=$(word 3,$(subst _, ,$*)) -DCTN_DV_EXP=$(word 4,$(subst _, ,$*)) $< -o $@
+	  -DCTN_DV_NC=$(word 2,$(subst _, ,$*)) -DCTN_DV_CJ=$(word 3,$(subst _, ,$*)) -DCTN_DV_CJN=$(word 3,$(subst _, ,$*)) \
+	  -DCTN_DV_EXP=$(word 4,$(subst _, ,$*)) -DCTN_DV_LA=$(word 5,$(subst _, ,$*)) $< -o $@
 
 .PHONY: dualwsnv
 .PHONY: dualwsdbg

@@ -42,7 +42,8 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 constexpr int DV_TM = 32;                        // frame rows per tile
 // column waves: 8 (64 dW2 accumulators each, 4 waves per SIMD, 128 VGPRs per wave) or 4
-// (128 accumulators each, 3 waves per SIMD, 168 VGPRs per wave)
+// (128 accumulators each, 3 waves per SIMD, 168 VGPRs per wave; measured slower: 86-91 us
+// at CJ=2 against 84 at 8 waves, CJ=1)
 #ifndef CTN_DV_NC
 #define CTN_DV_NC 8
 #endif
@@ -90,7 +91,7 @@ static_assert(DV_PF_CLN >= 1 && DV_PF_CLN <= DV_NSL - 1, "ring look-ahead (cLN)"
 #endif
 constexpr int DV_CJ = CTN_DV_CJ, DV_CI = 16 / DV_CJ;
 static_assert(DV_CJ == 1 || DV_CJ == 2 || DV_CJ == 4, "column blocks per column wave");
-// N image (CTN_DV_NIMG=1, default; RAWB=1 only): the row waves, which already apply PReLU +
+// N image (CTN_DV_NIMG=1, experiment, off; RAWB=1 only): the row waves, which already apply PReLU +
 // norm to the raw d of their 16-byte granules in the epilogue, also write op(d) =
 // gamma2 * hat a2 + beta2 (bf16) over that raw d in the B image, and the column waves wait
 // for the four row waves' DONE of the tile instead of FULL and read op(d) fragments without
@@ -98,7 +99,10 @@ static_assert(DV_CJ == 1 || DV_CJ == 2 || DV_CJ == 4, "column blocks per column 
 // their transform chain and the B statistics, and their split is free to read the fewest
 // fragments (CTN_DV_CJN column blocks per wave).  op(d) is rounded from fmaf(hat a, gamma,
 // beta) instead of fmaf(a - mean, rstd * gamma, beta): dW2 differs from the NIMG=0 kernel
-// in the last bits of some bf16 operands; C and the statistics are unchanged.
+// in the last bits of some bf16 operands; C and the statistics are unchanged.  Measured
+// slower (microbenchmark, bench shape: 113-115 us at 8 column waves, 85-91 at 4, against
+// 83-84 us without): the column waves then wait for the row waves' whole
+// tile, and the row waves, which set the pace, carry the extra work.
 #ifndef CTN_DV_NIMG
 #define CTN_DV_NIMG 0
 #endif

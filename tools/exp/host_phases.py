@@ -1,4 +1,6 @@
-"""Host-side issue time per phase of the bench step (no syncs added inside the step):
+"""Host-side issue time per phase of the bench step (no syncs added inside the step;
+--sync drains the GPU before each phase, so each phase's host time is free of queue
+back-pressure):
 a phase whose host time jumps to GPU-time scale contains a synchronization.  Also runs
 three steps under torch.cuda.set_sync_debug_mode("warn") to name synchronizing calls."""
 import sys, time, warnings
@@ -20,17 +22,31 @@ mix, src = synthetic.speech_like(M, C, T, 1234)
 mix, src = mix.to(dev), src.to(dev)
 lens = torch.full((M,), T, dtype=torch.int64, device=dev)
 ph = {}
+SYNC = "--sync" in sys.argv   # drain the GPU before each phase: host cost without queue back-pressure
+
+
 def step(rec):
-    t = [time.perf_counter()]
-    est = model(mix); t.append(time.perf_counter())
-    loss = pc.cal_loss(src, est, lens)[0]; t.append(time.perf_counter())
-    opt.zero_grad(set_to_none=True); t.append(time.perf_counter())
-    loss.backward(); t.append(time.perf_counter())
-    ctn_optim.clip_grad_norm_(model.parameters(), 5.0); t.append(time.perf_counter())
-    opt.step(); t.append(time.perf_counter())
+    times = []
+
+    def run(name, fn):
+        if SYNC:
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        r = fn()
+        times.append((name, (time.perf_counter() - t0) * 1e3))
+        return r
+
+    est = run("forward", lambda: model(mix))
+    loss = run("loss", lambda: pc.cal_loss(src, est, lens)[0])
+    run("zero_grad", lambda: opt.zero_grad(set_to_none=True))
+    run("backward", lambda: loss.backward())
+    run("clip", lambda: ctn_optim.clip_grad_norm_(model.parameters(), 5.0))
+    run("adam", lambda: opt.step())
     if rec:
-        for i, n in enumerate(["forward", "loss", "zero_grad", "backward", "clip", "adam"]):
-            ph.setdefault(n, []).append((t[i + 1] - t[i]) * 1e3)
+        for n, v in times:
+            ph.setdefault(n, []).append(v)
+
+
 for _ in range(5):
     step(False)
 torch.cuda.synchronize()
@@ -58,3 +74,4 @@ for x in w:
         seen.add(k)
         print("SYNC:", k)
 print(f"{len(w)} sync warnings in 2 steps")
+print("optimizer fast paths:", ctn_optim.FAST_STATS, "(sync mode)" if SYNC else "")
