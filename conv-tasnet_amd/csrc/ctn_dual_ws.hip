@@ -118,6 +118,12 @@ static_assert(CTN_DV_CJN == 1 || CTN_DV_CJN == 2 || CTN_DV_CJN == 4 || CTN_DV_CJ
 constexpr int DV_CJC = CTN_DV_CJC;
 static_assert(DV_CJC == 1 || DV_CJC == 2 || DV_CJC == 4, "column blocks per column wave (COLS)");
 
+// cLN: combine the four row waves' per-row statistics partials in LDS before storing
+// (S entries per row instead of 4 S)
+#ifndef CTN_DV_CLNC
+#define CTN_DV_CLNC 1
+#endif
+
 // Row waves: A fragments read LA k-steps ahead of their MFMAs
 #ifndef CTN_DV_LA
 #define CTN_DV_LA 1
@@ -247,6 +253,11 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
   __shared__ __attribute__((aligned(16))) uint32_t fl_full[NSL][4];   // per memory wave
   __shared__ __attribute__((aligned(16))) uint32_t fl_done[NSL][ND];   // per row / column wave
   __shared__ __attribute__((aligned(16))) float sgb[2][NS];            // gamma2 / beta2 of the slice
+  // cLN (CTN_DV_CLNC): the four row waves' per-row partials of a tile, two tiles deep, and
+  // one generation word per (buffer, row wave)
+  constexpr bool CLNC = NK == NORM_CLN && !COLS && CTN_DV_CLNC;
+  __shared__ __attribute__((aligned(16))) double2 cln_scr[CLNC ? 2 : 1][CLNC ? DV_NR * DV_TM : 1];
+  __shared__ __attribute__((aligned(16))) uint32_t fl_rows[2][4];
 
   // wave id through readfirstlane: wave-uniform to the compiler, so per-role pointers and
   // offsets live in SGPRs (the row waves are at the 128-VGPR limit of 4 waves per SIMD)
@@ -274,6 +285,7 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
 
   if (tid < NSL * 4) (&fl_full[0][0])[tid] = 0u;
   else if (tid < NSL * (4 + ND)) (&fl_done[0][0])[tid - NSL * 4] = 0u;
+  else if (tid < NSL * (4 + ND) + 8) (&fl_rows[0][0])[tid - NSL * (4 + ND)] = 0u;
   if constexpr (!COLS)
     if (tid < 2 * NS) sgb[tid / NS][tid % NS] = (tid < NS ? p.bop.gamma : p.bop.beta)[n0 + tid % NS];
   __syncthreads();
@@ -439,6 +451,31 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
             }
             run_s += (double)(s1[0] + s1[1]);
             run_q += (double)(q1[0] + q1[1]);
+          } else if constexpr (CLNC) {
+            // per-row partial over this wave's 32 channels into LDS; once all four row
+            // waves have written theirs, wave r sums rows 8r .. 8r+7 over the waves in
+            // order 0..3 and stores one entry per (row, slice): a quarter of the
+            // statistics bytes the finalize reads
+            const int k = t - t0, bsel = k & 1;
+            const uint32_t rgen = (uint32_t)(k >> 1) + 1u;
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb) {
+              const float s = xsum_rows(s1[rb]), ss = xsum_rows(q1[rb]);
+              if (lg == 0) cln_scr[bsel][r * TM + 16 * rb + lr] = make_double2((double)s, (double)ss);
+            }
+            dv_signal(&fl_rows[bsel][r], rgen);
+            dv_wait<4>(fl_rows[bsel], rgen, p.err);
+            if (lane < 8) {
+              const int row = 8 * r + lane;
+              double s = 0.0, ss = 0.0;
+#pragma unroll
+              for (int w = 0; w < DV_NR; ++w) {
+                const double2 v = cln_scr[bsel][w * TM + row];
+                s += v.x;
+                ss += v.y;
+              }
+              p.grp_slab[((size_t)t * TM + row) * S + sl] = make_double2(s, ss);
+            }
           } else {
             // per-row partial over this wave's 32 channels (the four lane groups): one
             // entry per (row, slice, row wave), summed in that order by the finalize
@@ -738,6 +775,9 @@ bool gemm_dual_ws_enabled() {
   const char* e = getenv("CTN_DUAL_WS");
   return e ? atoi(e) != 0 : true;
 }
+
+// cLN statistics entries per (row, slice) the kernel stores (gemm_dual_group_parts)
+int dual_ws_cln_parts_per_slice() { return CTN_DV_CLNC ? 1 : DV_NR; }
 
 bool gemm_dual_ws_eligible(const GemmDual& p) {
   if (!gemm_dual_ws_enabled()) return false;

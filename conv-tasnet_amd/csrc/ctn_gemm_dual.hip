@@ -643,7 +643,8 @@ WsRuns gemm_dual_runs(const GemmDual& p) {
 int gemm_dual_group_parts(const GemmDual& p) {
   int kb, nsb, nbw;
   dual_shape(p.Kred, p.Nout, &kb, &nsb, &nbw);
-  if (p.norm != NORM_GLN) return dual_slices(p) * (gemm_dual_ws_eligible(p) ? 4 : nsb / nbw);   // per (slice, row wave)
+  if (p.norm != NORM_GLN)   // per (slice, row wave), or per slice (ctn_dual_ws.hip, CTN_DV_CLNC)
+    return dual_slices(p) * (gemm_dual_ws_eligible(p) ? dual_ws_cln_parts_per_slice() : nsb / nbw);
   const WsRuns w = gemm_dual_runs(p);
   const long entries = (long)w.grid * w.waves * w.kmax;
   return (int)((entries + p.g.M - 1) / p.g.M);

@@ -123,6 +123,7 @@ struct GemmDual {
 bool gemm_dual_eligible(DType dt, const GemmDual& p);
 int gemm_dual_ranges(const GemmDual& p);
 int gemm_dual_group_parts(const GemmDual& p);
+int dual_ws_cln_parts_per_slice();   // ctn_dual_ws.hip: cLN statistics entries per (row, slice)
 StatFold gemm_dual_stat_fold(const GemmDual& p, const double2* slab, double cnt, float eps, int mode,
                              float2* out);
 hipError_t launch_gemm_dual(const GemmDual& p, hipStream_t s);
