@@ -890,7 +890,7 @@ static int tb_backward(const ctn_tblock_desc* d, const ctn_tblock_params* p, con
     CTN_HIP(launch_gemm_cols(dt, c2, s));
   }
   const bool fold = d->norm_type == CTN_NORM_GLN;   // gLN: consumers finalize the sums (StatFold)
-  if (!fold) CTN_HIP(launch_stats_finalize(L.slabA, G, L.partsA, cnt, 1, 0.f, L.sums2, s));
+
   // (c) depthwise backward -> G2 = dL/d(hat a1), norm1 sums, column partials (gamma1/beta1,
   //     wd, gamma2/beta2, alpha2)
   DwArgs da{};
@@ -905,6 +905,14 @@ static int tb_backward(const ctn_tblock_desc* d, const ctn_tblock_params* p, con
                      : gemm_rows_stat_fold(dt, ga, L.slabA, cnt, 0.f, 1, nullptr);
   else
     da.sm1_out = L.sums1;   // cLN: per-row norm-1 backward means final in the depthwise kernel
+  // cLN: the wave-item depthwise backward folds the dual's per-row partials itself (at most
+  // 4 per row: ctn_dual_ws.hip CTN_DV_CLNC) instead of a finalize launch
+  if (!fold) {
+    if (dualA && L.partsA <= 4 && dw_wave_eligible(dt, da))
+      da.f_sm2 = gemm_dual_stat_fold(duA, L.slabA, cnt, 0.f, 1, nullptr);
+    else
+      CTN_HIP(launch_stats_finalize(L.slabA, G, L.partsA, cnt, 1, 0.f, L.sums2, s));
+  }
   {
     TimedScope ts(CTN_TIMER_DW_BWD, s);
     CTN_HIP(launch_dw_bwd(dt, da, s));
@@ -1422,7 +1430,7 @@ static int pit_chunks(int T) {
   return c < 1 ? 1 : (c > 64 ? 64 : c);
 }
 
-constexpr int PIT_CMAX = 8;   // C! = 40,320 permutations
+constexpr int PIT_CMAX = 16;   // C <= 10: all C! permutations; 11..16: assignment (ctn_pit.hip)
 
 static void pit_perms(PitArgs& a) {
   int p[4] = {0, 1, 2, 3};

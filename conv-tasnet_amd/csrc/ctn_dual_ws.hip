@@ -89,7 +89,7 @@ static_assert(DV_PF_CLN >= 1 && DV_PF_CLN <= DV_NSL - 1, "ring look-ahead (cLN)"
 #ifndef CTN_DV_CJ
 #define CTN_DV_CJ 1
 #endif
-constexpr int DV_CJ = CTN_DV_CJ, DV_CI = 16 / DV_CJ;
+constexpr int DV_CJ = CTN_DV_CJ;
 static_assert(DV_CJ == 1 || DV_CJ == 2 || DV_CJ == 4, "column blocks per column wave");
 // N image (CTN_DV_NIMG=1, experiment, off; RAWB=1 only): the row waves, which already apply PReLU +
 // norm to the raw d of their 16-byte granules in the epilogue, also write op(d) =

@@ -349,16 +349,41 @@ __global__ __launch_bounds__(256, 2) void dw_bwd_wave_kernel(DwArgs a) {
   constexpr int CB = 63;
   float2 bst2 = make_float2(0.f, 0.f), bsm2 = bst2, bst1 = bst2, nst2 = bst2, nsm2 = bst2, nst1 = bst2;
   int bbase = it.j0;
+  // cLN norm-2 backward means: final (a.sm2), or folded here from the dual GEMM's per-row
+  // partials (a.f_sm2: dense, at most 4 per row; the finalize launch's arithmetic: parts
+  // summed in order from 0, divided by cnt in fp64, bit-identical).  A batch's raw parts
+  // are loaded with the batch and summed when it becomes current.
+  const StatFold& fs = a.f_sm2;
+  const bool fsm = NK == NORM_CLN && fs.slab != nullptr;
+  double2 nsmp[4];
+  auto sm_fold = [&](const double2* v) {
+    double s = 0.0, ss = 0.0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (q < fs.parts) s += v[q].x, ss += v[q].y;
+    return make_float2((float)(s / fs.cnt), (float)(ss / fs.cnt));
+  };
+  auto sm_load = [&](int row, double2* v) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = q < fs.parts ? fs.slab[(size_t)row * fs.parts + q] : make_double2(0.0, 0.0);
+  };
+  auto sm_row = [&](int row) {   // one row, outside the batches (prologue)
+    if (!fsm) return a.sm2[row];
+    double2 v[4];
+    sm_load(row, v);
+    return sm_fold(v);
+  };
   auto batch_fetch = [&](int jb) {
     const int rgw = row_at(jb + lane + GT), rhw = row_at(jb + lane);
     nst2 = a.st2[rgw];
-    nsm2 = a.sm2[rgw];
+    if (fsm) sm_load(rgw, nsmp);
+    else nsm2 = a.sm2[rgw];
     nst1 = a.st1[rhw];
   };
   auto batch_next = [&]() {   // the prefetched batch becomes current; fetch the one after
     bbase += CB;
     bst2 = nst2;
-    bsm2 = nsm2;
+    bsm2 = fsm ? sm_fold(nsmp) : nsm2;
     bst1 = nst1;
     batch_fetch(bbase + CB);
   };
@@ -423,7 +448,7 @@ __global__ __launch_bounds__(256, 2) void dw_bwd_wave_kernel(DwArgs a) {
       sm = bcast(bsm2, j);
     } else {
       st = a.st2[row];
-      sm = a.sm2[row];
+      sm = sm_row(row);
     }
   };
 

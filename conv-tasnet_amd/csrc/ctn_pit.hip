@@ -12,10 +12,17 @@
 // pit_bwd   : dL/dest[m][i][t] = scale_m (alpha s_j[t] + beta e_i[t] + offset), t < length.
 //
 // C <= 4: pit_final is one workgroup, one thread per utterance, the C! <= 24
-// permutations from a table in the kernel arguments.  5 <= C <= 8 (C! up to 40,320):
+// permutations from a table in the kernel arguments.  5 <= C <= 10 (C! up to 3,628,800):
 // pit_final_wide runs one workgroup per utterance whose threads split the
 // permutation indices (each decoded from its lexicographic rank, the order of
 // itertools.permutations), then pit_loss sums the utterances' maxima.
+// 11 <= C <= 16: C! (up to 2.1e13) is past what the reference itself can enumerate (its
+// one-hot table, pit_criterion.py:66-69, needs C!*C*C floats); the maximum of
+// sum_i snr[i][perm[i]] over permutations is a linear assignment, solved exactly by the
+// Hungarian algorithm in fp64 (pit_assign_max), and best_perm is that permutation's
+// lexicographic rank.  Exact ties between permutations may resolve to a different optimum
+// than the reference's first-in-order argmax.  C > 8 takes its statistics from
+// pit_stats_wide (runtime C, the chunk staged in LDS, one accumulator per value).
 #include "ctn_codec.h"
 #include "ctn_common.h"
 
@@ -139,6 +146,115 @@ __global__ __launch_bounds__(256) void pit_final_kernel(PitArgs a) {
   if (threadIdx.x == 0) a.loss[0] = (float)(-l1[0] / a.M);
 }
 
+// C > 8: the same per-(utterance, chunk) sums as pit_stats_kernel for a runtime C <= CW,
+// with C*(C+5) values: the chunk is staged through LDS 256 samples at a time and each
+// thread owns one or two of the values, summed in sample order (fp64)
+template <int CW>
+__global__ __launch_bounds__(256) void pit_stats_wide_kernel(PitArgs a) {
+  constexpr int SUB = 256;
+  __shared__ float se[CW][SUB], sv[CW][SUB];
+  const int C = a.C, NV = 5 * C + C * C;
+  const int m = blockIdx.y, chunk = blockIdx.x, tid = threadIdx.x;
+  const int T = a.T;
+  const long len = a.lengths[m];
+  const int span = (T + a.chunks - 1) / a.chunks;
+  const int t0 = chunk * span, t1 = t0 + span < T ? t0 + span : T;
+  // value v: kind (0 SE, 1 SSv, 2 SSa, 3 EE, 4 TT, 5 ES), estimate i, source j
+  int kind[2], vi[2], vj[2];
+  double acc[2] = {0.0, 0.0};
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int v = tid + 256 * u;
+    kind[u] = v < 5 * C ? v / C : (v < NV ? 5 : -1);
+    vi[u] = v < 5 * C ? v % C : (v - 5 * C) / C;
+    vj[u] = v < 5 * C ? v % C : (v - 5 * C) % C;
+  }
+  for (int tb = t0; tb < t1; tb += SUB) {
+    __syncthreads();
+    for (int idx = tid; idx < C * SUB; idx += 256) {
+      const int i = idx / SUB, tt = idx % SUB, t = tb + tt;
+      const bool inT = t < t1;
+      se[i][tt] = inT && t < len ? a.est[((size_t)m * C + i) * T + t] : 0.f;
+      sv[i][tt] = inT ? a.src[((size_t)m * C + i) * T + t] : 0.f;
+    }
+    __syncthreads();
+    const int n = t1 - tb < SUB ? t1 - tb : SUB;
+    const int nin = len - tb <= 0 ? 0 : (len - tb < n ? (int)(len - tb) : n);   // samples with t < len
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = vi[u], j = vj[u];
+      double x = acc[u];
+      switch (kind[u]) {
+        case 0: for (int tt = 0; tt < n; ++tt) x += (double)se[i][tt]; break;                        // SE
+        case 1: for (int tt = 0; tt < nin; ++tt) x += (double)sv[i][tt]; break;                      // SSv
+        case 2: for (int tt = 0; tt < n; ++tt) x += (double)sv[i][tt]; break;                        // SSa
+        case 3: for (int tt = 0; tt < n; ++tt) x += (double)se[i][tt] * (double)se[i][tt]; break;    // EE
+        case 4: for (int tt = 0; tt < nin; ++tt) x += (double)sv[i][tt] * (double)sv[i][tt]; break;  // TT
+        case 5: for (int tt = 0; tt < nin; ++tt) x += (double)se[i][tt] * (double)sv[j][tt]; break;  // ES
+        default: break;
+      }
+      acc[u] = x;
+    }
+  }
+  double* o = a.slab + ((size_t)m * a.chunks + chunk) * NV;
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+    if (kind[u] >= 0) o[tid + 256 * u] = acc[u];
+}
+
+// maximum-weight perfect matching of estimates (rows) to sources (columns) of w, in fp64:
+// the Hungarian algorithm with potentials (minimising -w), O(C^3); perm[i] = source of i
+template <int C>
+CTN_DEV void pit_assign_max(const double (*w)[C], int* perm) {
+  double u[C + 1], v[C + 1], minv[C + 1];
+  int p[C + 1], way[C + 1];
+  bool used[C + 1];
+  for (int j = 0; j <= C; ++j) u[j] = v[j] = 0.0, p[j] = way[j] = 0;
+  for (int i = 1; i <= C; ++i) {
+    p[0] = i;
+    int j0 = 0;
+    for (int j = 0; j <= C; ++j) minv[j] = 1e300, used[j] = false;
+    do {
+      used[j0] = true;
+      const int i0 = p[j0];
+      double delta = 1e300;
+      int j1 = 0;
+      for (int j = 1; j <= C; ++j)
+        if (!used[j]) {
+          const double cur = -w[i0 - 1][j - 1] - u[i0] - v[j];
+          if (cur < minv[j]) minv[j] = cur, way[j] = j0;
+          if (minv[j] < delta) delta = minv[j], j1 = j;
+        }
+      for (int j = 0; j <= C; ++j) {
+        if (used[j]) u[p[j]] += delta, v[j] -= delta;
+        else minv[j] -= delta;
+      }
+      j0 = j1;
+    } while (p[j0] != 0);
+    do {
+      const int j1 = way[j0];
+      p[j0] = p[j1];
+      j0 = j1;
+    } while (j0);
+  }
+  for (int j = 1; j <= C; ++j) perm[p[j] - 1] = j - 1;
+}
+
+// lexicographic rank of a permutation of range(C) (itertools.permutations order)
+CTN_DEV long pit_rank(const int* perm, int C) {
+  long r = 0, f = 1;
+  for (int i = 2; i < C; ++i) f *= i;   // (C-1)!
+  unsigned used = 0;
+  for (int i = 0; i < C; ++i) {
+    int smaller = 0;
+    for (int v = 0; v < perm[i]; ++v) smaller += !((used >> v) & 1u);
+    used |= 1u << perm[i];
+    r += smaller * f;
+    if (C - 1 - i > 0) f /= C - 1 - i;
+  }
+  return r;
+}
+
 // permutation of range(C) with lexicographic rank p (itertools.permutations order)
 CTN_DEV void pit_decode(long p, int C, int* out) {
   long f = 1;
@@ -156,7 +272,7 @@ CTN_DEV void pit_decode(long p, int C, int* out) {
   }
 }
 
-// 5 <= C <= 8: one workgroup per utterance (pit_criterion.py:41-75 for one row)
+// 5 <= C <= 16: one workgroup per utterance (pit_criterion.py:41-75 for one row)
 template <int C>
 __global__ __launch_bounds__(256) void pit_final_wide_kernel(PitArgs a) {
   constexpr int NV = 5 * C + C * C;
@@ -187,24 +303,35 @@ __global__ __launch_bounds__(256) void pit_final_wide_kernel(PitArgs a) {
     if (j == 0) eb[i] = ebi;
   }
   __syncthreads();
-  long nperm = 1;
-  for (int i = 2; i <= C; ++i) nperm *= i;
   double best = -1e300;
-  long bi = nperm;
-  for (long p = tid; p < nperm; p += 256) {
-    int pm[C];
-    pit_decode(p, C, pm);
-    double sv = 0.0;
+  long bi = 0;
+  if constexpr (C <= 10) {
+    long nperm = 1;
+    for (int i = 2; i <= C; ++i) nperm *= i;
+    bi = nperm;
+    for (long p = tid; p < nperm; p += 256) {
+      int pm[C];
+      pit_decode(p, C, pm);
+      double sv = 0.0;
 #pragma unroll
-    for (int i = 0; i < C; ++i) sv += snr[i][pm[i]];
-    if (sv > best) { best = sv; bi = p; }   // ascending p: first maximum of this thread
+      for (int i = 0; i < C; ++i) sv += snr[i][pm[i]];
+      if (sv > best) { best = sv; bi = p; }   // ascending p: first maximum of this thread
+    }
+    bv[tid] = best;
+    bp[tid] = bi;
+    __syncthreads();
   }
-  bv[tid] = best;
-  bp[tid] = bi;
-  __syncthreads();
   if (tid == 0) {
-    for (int t = 1; t < 256; ++t)   // first maximum over all ranks, like torch.argmax
-      if (bv[t] > best || (bv[t] == best && bp[t] < bi)) { best = bv[t]; bi = bp[t]; }
+    if constexpr (C <= 10) {
+      for (int t = 1; t < 256; ++t)   // first maximum over all ranks, like torch.argmax
+        if (bv[t] > best || (bv[t] == best && bp[t] < bi)) { best = bv[t]; bi = bp[t]; }
+    } else {   // the same maximum as a linear assignment
+      int pm[C];
+      pit_assign_max<C>(snr, pm);
+      best = 0.0;
+      for (int i = 0; i < C; ++i) best += snr[i][pm[i]];
+      bi = pit_rank(pm, C);
+    }
     const double ms = best / C;
     a.max_snr[m] = (float)ms;
     a.best[m] = bi;
@@ -286,9 +413,12 @@ __global__ __launch_bounds__(256) void pit_bwd_kernel(PitArgs a) {
   }
 }
 
+constexpr int PIT_CW = 16;   // largest C (pit_stats_wide_kernel's staging arrays)
+
 template <int C>
 static hipError_t pit_fwd_c(const PitArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(pit_stats_kernel<C>, dim3(a.chunks, a.M), dim3(256), 0, s, a);
+  if constexpr (C <= 8) hipLaunchKernelGGL(pit_stats_kernel<C>, dim3(a.chunks, a.M), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(pit_stats_wide_kernel<PIT_CW>, dim3(a.chunks, a.M), dim3(256), 0, s, a);
   if constexpr (C <= 4) {
     hipLaunchKernelGGL(pit_final_kernel<C>, dim3(1), dim3(256), 0, s, a);
   } else {
@@ -322,6 +452,14 @@ hipError_t launch_pit_forward(const PitArgs& a, hipStream_t s) {
     case 6: return pit_fwd_c<6>(a, s);
     case 7: return pit_fwd_c<7>(a, s);
     case 8: return pit_fwd_c<8>(a, s);
+    case 9: return pit_fwd_c<9>(a, s);
+    case 10: return pit_fwd_c<10>(a, s);
+    case 11: return pit_fwd_c<11>(a, s);
+    case 12: return pit_fwd_c<12>(a, s);
+    case 13: return pit_fwd_c<13>(a, s);
+    case 14: return pit_fwd_c<14>(a, s);
+    case 15: return pit_fwd_c<15>(a, s);
+    case 16: return pit_fwd_c<16>(a, s);
   }
   return hipErrorInvalidValue;
 }
@@ -336,6 +474,14 @@ hipError_t launch_pit_backward(const PitArgs& a, hipStream_t s) {
     case 6: return pit_bwd_c<6>(a, s);
     case 7: return pit_bwd_c<7>(a, s);
     case 8: return pit_bwd_c<8>(a, s);
+    case 9: return pit_bwd_c<9>(a, s);
+    case 10: return pit_bwd_c<10>(a, s);
+    case 11: return pit_bwd_c<11>(a, s);
+    case 12: return pit_bwd_c<12>(a, s);
+    case 13: return pit_bwd_c<13>(a, s);
+    case 14: return pit_bwd_c<14>(a, s);
+    case 15: return pit_bwd_c<15>(a, s);
+    case 16: return pit_bwd_c<16>(a, s);
   }
   return hipErrorInvalidValue;
 }

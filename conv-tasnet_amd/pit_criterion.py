@@ -24,6 +24,9 @@ def _perms(C, device):
     """range(C)'s permutations as a device tensor, built once per (C, device): a tensor
     made from a host list is a synchronous pageable copy, which in the training step
     stalled the host until the GPU had finished the forward pass."""
+    if C > 10:   # 11! rows x C is 0.4 GB and grows C-fold: the reference's table stops being buildable
+        raise L.CtnLibraryError(f"cal_si_snr_with_pit: the permutation table of C={C} speakers has {C}! "
+                                "rows; cal_loss (assignment search on the device) supports C <= 16")
     key = (C, str(device))
     t = _PERMS.get(key)
     if t is None:

@@ -207,8 +207,11 @@ int ctn_decoder_backward(const ctn_codec_desc* d, const void* x_last, const void
  * get_mask, src/pit_criterion.py:12-113.  `est` is masked in place beyond
  * each length (:37-38); `reordered` (nullable) keeps the reference's
  * perm-not-inverse indexing (:91-97).  `coef` [M*C*4] is saved for backward.
- * 1 <= C <= 8 (all C! permutations, :66; 0 workspace bytes / CTN_ERR_UNSUPPORTED
- * beyond); the encoder/decoder descriptors accept the same range.
+ * 1 <= C <= 16 (0 workspace bytes / CTN_ERR_UNSUPPORTED beyond): C <= 10 searches all C!
+ * permutations (:66) and keeps the first maximum (torch.argmax); 11 <= C <= 16, past what
+ * the reference's C!-row one-hot table can hold, solves the same maximum as a linear
+ * assignment (Hungarian, fp64) and reports its lexicographic rank in best_perm (exact ties
+ * may pick another optimal permutation).  The encoder/decoder descriptors accept 1..8.
  * ------------------------------------------------------------------------- */
 typedef struct { int32_t M, C, T; } ctn_pit_desc;
 size_t ctn_pit_workspace_bytes(const ctn_pit_desc* d);

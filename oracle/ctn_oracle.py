@@ -269,6 +269,54 @@ def get_mask(source, lengths):
     return (t < lengths.view(-1, 1)).to(source.dtype).unsqueeze(1)
 
 
+def si_snr_pairwise(source, est, lengths):
+    """pit_criterion.py:36-62: the pairwise SI-SNR matrix snr[b, i, j] (estimate i against
+    source j) and the masked estimate."""
+    assert source.shape == est.shape
+    Bsz, C, T = source.shape
+    mask = get_mask(source, lengths)
+    est = est * mask
+    n = lengths.view(-1, 1, 1).to(source.dtype)
+    zt = (source - source.sum(2, keepdim=True) / n) * mask
+    ze = (est - est.sum(2, keepdim=True) / n) * mask
+    dot = torch.einsum("bit,bjt->bij", ze, zt)
+    e_t = (zt ** 2).sum(2) + EPS
+    proj = dot.unsqueeze(-1) * zt.unsqueeze(1) / e_t.view(Bsz, 1, C, 1)
+    noise = ze.unsqueeze(2) - proj
+    ratio = (proj ** 2).sum(3) / ((noise ** 2).sum(3) + EPS)
+    return 10 * torch.log10(ratio + EPS), est
+
+
+def perm_rank(perm):
+    """Lexicographic rank of a permutation of range(C) (the itertools.permutations order
+    the reference indexes its table in, pit_criterion.py:66)."""
+    C, r, used = len(perm), 0, set()
+    for i, p in enumerate(perm):
+        r += sum(1 for v in range(p) if v not in used) * math.factorial(C - 1 - i)
+        used.add(p)
+    return r
+
+
+def si_snr_pit_assign(source, est, lengths):
+    """The maximum of cal_si_snr_with_pit's permutation sums (pit_criterion.py:66-75) for any
+    C as a linear assignment on the pairwise SI-SNR (scipy.optimize.linear_sum_assignment,
+    maximize): equal to the reference's argmax over C! permutations except on exact ties,
+    and usable where the reference's C!-row table is not (C > 10).  Returns (max_snr [B,1],
+    perm [B,C] (estimate i -> source perm[i]), rank [B], est_masked)."""
+    from scipy.optimize import linear_sum_assignment
+    snr, est_m = si_snr_pairwise(source, est, lengths)
+    Bsz, C, _ = snr.shape
+    perms, ranks, vals = [], [], []
+    for b in range(Bsz):
+        rows, cols = linear_sum_assignment(snr[b].detach().double().numpy(), maximize=True)
+        p = [int(c) for _, c in sorted(zip(rows, cols))]
+        perms.append(p)
+        ranks.append(perm_rank(p))
+        vals.append(snr[b, torch.arange(C), torch.tensor(p)].sum())
+    max_snr = torch.stack(vals).view(Bsz, 1) / C
+    return max_snr, torch.tensor(perms), torch.tensor(ranks), est_m
+
+
 def si_snr_pit(source, est, lengths):
     """cal_si_snr_with_pit (pit_criterion.py:27-76), returns (max_snr, perms, idx, est_masked).
 

@@ -5,6 +5,7 @@ Run from the repo root:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_gold
 
 pit_wide.npz   : cal_loss (pit_criterion.py:12-113) for C = 5, 6, 8 — C! = 120, 720,
                  40,320 permutations (pit_criterion.py:66) — equal and unequal lengths
+pit_c9_10.npz  : the same at C = 9 and 10 (python tests/golden/make_golden_wide.py --c9)
 model_5spk.npz : a full ConvTasNet forward + PIT loss + backward at C = 5 (small dims)
 """
 import numpy as np
@@ -39,8 +40,43 @@ def pit_wide_fixtures():
     mg.save("pit_wide.npz", **out)
 
 
+def pit_c9_c10_fixtures():
+    """pit_c9_10.npz: cal_loss at C = 9 and 10 (C! = 362,880 and 3,628,800 permutations,
+    the reference's own one-hot enumeration: 1.45 GB at C = 10), equal and unequal
+    lengths; beyond C = 10 the reference cannot build its table (tests/test_gpu_pit_wide.py
+    checks the assignment path against scipy on the oracle's pairwise SI-SNR instead)."""
+    rng = np.random.default_rng(911)
+    out = {}
+    for C, T in ((9, 300), (10, 240)):
+        for tag, lens in (("eq", [T, T]), ("neq", [T, T * 2 // 3])):
+            src = rng.standard_normal((2, C, T)).astype(np.float32)
+            for b, l in enumerate(lens):
+                src[b, :, l:] = 0
+            perm = [list(rng.permutation(C)) for _ in range(2)]
+            est = np.stack([src[b, perm[b]] for b in range(2)]) * 0.8 + \
+                0.5 * rng.standard_normal((2, C, T)).astype(np.float32) + 0.3
+            s = torch.from_numpy(src)
+            e = torch.from_numpy(est.astype(np.float32)).requires_grad_(True)
+            e2 = e * 1.0
+            lengths = torch.tensor(lens)
+            loss, max_snr, est_m, reord = mg.ref_pit.cal_loss(s, e2, lengths)
+            loss.backward()
+            _, _, idx = mg.ref_pit.cal_si_snr_with_pit(s, (e * 1.0).detach(), lengths)
+            k = f"pit.C{C}.{tag}"
+            out.update({k + ".src": s, k + ".est": e.detach(), k + ".len": lengths,
+                        k + ".loss": loss.detach(), k + ".max_snr": max_snr.detach(),
+                        k + ".est_m": est_m.detach(), k + ".reord": reord.detach(),
+                        k + ".gest": e.grad, k + ".idx": idx, k + ".perm": np.array(perm)})
+    mg.save("pit_c9_10.npz", **out)
+
+
 if __name__ == "__main__":
+    import sys
     torch.manual_seed(0)
+    if "--c9" in sys.argv:   # only the C = 9, 10 fixtures (round 5)
+        pit_c9_c10_fixtures()
+        sys.exit(0)
     pit_wide_fixtures()
+    pit_c9_c10_fixtures()
     mg.model_fixture("model_5spk.npz", O.Cfg(64, 20, 64, 128, 3, 2, 2, 5), 2, 4000, 6,
                      lens=[4000, 3300], full=True)

@@ -83,8 +83,8 @@ def test_forward_rejects_null_and_small_workspace(lib):
     sv = L.TBlockSaved()
     assert lib.ctn_tblock_forward(ctypes.byref(d), ctypes.byref(p), None, None, ctypes.byref(sv), None, 0, None) == 1
     assert lib.ctn_pit_forward(None, None, None, None, None, None, None, None, None, None, 0, None) == 1
-    pd = L.PitDesc(2, 9, 100)
-    assert lib.ctn_pit_workspace_bytes(ctypes.byref(pd)) == 0          # C > 8 unsupported
+    pd = L.PitDesc(2, 17, 100)
+    assert lib.ctn_pit_workspace_bytes(ctypes.byref(pd)) == 0          # C > 16 unsupported
     pd = L.PitDesc(2, 8, 100)
     assert lib.ctn_pit_workspace_bytes(ctypes.byref(pd)) > 0           # C! = 40,320 permutations
 
@@ -172,3 +172,12 @@ def test_tblock_plan_bench_shape_and_2gb_fallback(lib):
     assert "gx" not in bwd or bwd["gx"] != "ws_n1bwd", bwd
     just_below = dict(M=655, K=3199, Kp=3200)  # 2,096,000 rows
     assert _plan(lib, 1, **just_below)["pairA"] == "dual_ws"
+
+
+def test_pit_speaker_range(lib):
+    """ctn_pit_workspace_bytes: 1..16 speakers (C <= 10 enumerated, 11..16 by assignment),
+    0 bytes (unsupported) beyond."""
+    import ctn_lib as L
+    for C, ok in ((1, True), (8, True), (9, True), (16, True), (17, False)):
+        n = lib.ctn_pit_workspace_bytes(ctypes.byref(L.PitDesc(4, C, 1000)))
+        assert (n > 0) == ok, (C, n)

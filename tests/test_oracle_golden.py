@@ -107,6 +107,37 @@ def test_pit(C, tag):
     close(est.grad, g[k + ".gest"], 1e-4, 1e-7)
 
 
+@pytest.mark.parametrize("C", [9, 10])
+@pytest.mark.parametrize("tag", ["eq", "neq"])
+def test_pit_assign_vs_reference_c9_c10(C, tag):
+    """The oracle's assignment form of the PIT maximum (si_snr_pit_assign, used to check
+    C > 10 where the reference cannot enumerate C!) against the reference captured at
+    C = 9, 10 (pit_c9_10.npz, make_golden_wide.py --c9): same maximum, same permutation
+    rank, same reordered estimate."""
+    g = load("pit_c9_10.npz")
+    k = f"pit.C{C}.{tag}"
+    max_snr, perm, rank, est_m = O.si_snr_pit_assign(T(g[k + ".src"]), T(g[k + ".est"]), T(g[k + ".len"]))
+    close(max_snr, g[k + ".max_snr"], 1e-5, 1e-5)
+    assert rank.tolist() == g[k + ".idx"].tolist()
+    reord = torch.stack([est_m[b, perm[b]] for b in range(est_m.shape[0])])
+    close(reord, g[k + ".reord"], 0, 0)
+
+
+def test_pit_assign_equals_enumeration_small_c():
+    """Assignment and the reference's enumeration (O.si_snr_pit) agree at C = 4..7 on random
+    inputs: same maximum and the same permutation rank."""
+    rng = np.random.default_rng(5)
+    for C in range(4, 8):
+        src = torch.from_numpy(rng.standard_normal((3, C, 200)).astype(np.float32))
+        est = src[:, torch.from_numpy(rng.permutation(C))] * 0.7 + \
+            torch.from_numpy(rng.standard_normal((3, C, 200)).astype(np.float32)) * 0.6
+        lens = torch.tensor([200, 150, 90])
+        m1, _, idx, _ = O.si_snr_pit(src, est, lens)
+        m2, _, rank, _ = O.si_snr_pit_assign(src, est, lens)
+        close(m2, m1, 1e-6, 1e-6)
+        assert rank.tolist() == idx.tolist()
+
+
 def test_sisnr():
     g = load("sisnr.npz")
     for c in range(2):
