@@ -1097,7 +1097,7 @@ static int codec_check(const ctn_codec_desc* d, bool need_b) {
   if (d->N % 8 || cg > 64 || (cg & (cg - 1)))
     return fail(CTN_ERR_UNSUPPORTED, "N=%d: need N/8 a power of two <= 64", d->N);
   if (need_b && (d->B % 8 || d->B < 8)) return fail(CTN_ERR_UNSUPPORTED, "B=%d must be a multiple of 8", d->B);
-  if (d->C < 1 || d->C > 8) return fail(CTN_ERR_UNSUPPORTED, "C=%d outside 1..8", d->C);
+  if (d->C < 1 || d->C > 16) return fail(CTN_ERR_UNSUPPORTED, "C=%d outside 1..16", d->C);
   if (d->mask_type < 0 || d->mask_type > 2) return fail(CTN_ERR_ARG, "mask_type %d", d->mask_type);
   if (d->dtype != CTN_DTYPE_F32 && d->dtype != CTN_DTYPE_BF16) return fail(CTN_ERR_ARG, "dtype %d", d->dtype);
   return CTN_OK;

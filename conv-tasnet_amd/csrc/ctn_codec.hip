@@ -174,11 +174,13 @@ __global__ __launch_bounds__(256) void enc_bwd_rows_kernel(CodecArgs a) {
 // ===========================================================================
 constexpr int FO_R = 16, FO_WGS = 512, FO_LMAX = 32;
 
-// LT: compile-time L (0: generic, <= FO_LMAX); CM: speakers held per row (4, or 8 for
-// 5 <= C <= 8, with FO_R / 2 rows per chunk so the staged rows stay within LDS)
+// LT: compile-time L (0: generic, <= FO_LMAX); CM: speakers held per row (4, 8 for
+// 5 <= C <= 8 with FO_R / 2 rows per chunk, or 16 for 9 <= C <= 16 with FO_R / 4, so the
+// staged rows stay within LDS)
+constexpr int fo_rows(int C) { return C > 8 ? FO_R / 4 : (C > 4 ? FO_R / 2 : FO_R); }
 template <typename T, int MODE, int LT, int CM = 4>
 __global__ __launch_bounds__(256) void frame_outer_kernel(CodecArgs a) {
-  constexpr int FO_R = CM > 4 ? ctn::FO_R / 2 : ctn::FO_R;
+  constexpr int FO_R = fo_rows(CM);
   extern __shared__ __attribute__((aligned(16))) float sm[];
   constexpr int LL = LT ? LT : FO_LMAX;
   const int N = a.N, L = LT ? LT : a.L, S = a.S, C = MODE == 0 ? 1 : a.C, K = a.K, Kp = a.Kp;
@@ -281,7 +283,7 @@ __global__ __launch_bounds__(256) void frame_outer_kernel(CodecArgs a) {
 // decoder forward: frames[m][c][k][l]  (fp32)
 // workgroup = DEC_RPB frame rows; src = w * act(score) staged in LDS [rows][C][N]
 // ===========================================================================
-template <typename T, int CM = 4>   // CM: speakers held per row (4 or 8)
+template <typename T, int CM = 4>   // CM: speakers held per row (4, 8 or 16)
 __global__ __launch_bounds__(256) void dec_fwd_kernel(CodecArgs a, int rpb) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int N = a.N, L = a.L, C = a.C, K = a.K, Kp = a.Kp;
@@ -349,7 +351,7 @@ __global__ __launch_bounds__(256) void ola_fwd_kernel(CodecArgs a) {
 // ===========================================================================
 // decoder backward (rows): gsrc = gframes . V ; gw = sum_c gsrc_c act_c ; gscore
 // ===========================================================================
-template <typename T, int CM = 4>   // CM: speakers held per row (4 or 8)
+template <typename T, int CM = 4>   // CM: speakers held per row (4, 8 or 16)
 __global__ __launch_bounds__(256) void dec_bwd_kernel(CodecArgs a, int rpb) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int N = a.N, L = a.L, C = a.C, S = a.S, K = a.K, Kp = a.Kp;
@@ -784,7 +786,7 @@ static unsigned dm_grid(const CodecArgs& a) {
 // ===========================================================================
 static bool codec_ok(const CodecArgs& a) {
   return a.N % 8 == 0 && a.N / 8 <= 64 && ((a.N / 8) & (a.N / 8 - 1)) == 0 && a.L >= 1 && a.L <= 32 &&
-         a.S >= 1 && a.C >= 1 && a.C <= 8 && a.Kp % EN_RPB == 0;
+         a.S >= 1 && a.C >= 1 && a.C <= 16 && a.Kp % EN_RPB == 0;
 }
 
 hipError_t launch_enc_fwd(DType dt, const CodecArgs& a, hipStream_t s) {
@@ -809,19 +811,20 @@ hipError_t launch_enc_bwd_rows(DType dt, const CodecArgs& a, hipStream_t s) {
 }
 
 int frame_outer_chunks(const CodecArgs& a, int C) {
-  const int n = a.M * (a.Kp / (C > 4 ? FO_R / 2 : FO_R));
+  const int n = a.M * (a.Kp / fo_rows(C));
   return n < FO_WGS ? n : FO_WGS;
 }
 
 hipError_t launch_frame_outer(DType dt, int mode, const CodecArgs& a, hipStream_t s) {
   if (!codec_ok(a) || a.Kp % FO_R || a.N > 512 || a.L > FO_LMAX) return hipErrorInvalidValue;
   const int C = mode == 0 ? 1 : a.C;
-  const int fr = C > 4 ? FO_R / 2 : FO_R;
+  const int fr = fo_rows(C);
   const size_t lds = ((size_t)fr * C * a.N + (size_t)C * (fr * a.S + a.L)) * sizeof(float);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   const dim3 g(frame_outer_chunks(a, C)), b(256);
 #define CTN_FO(T_, M_)                                                                                          \
-  if (C > 4) hipLaunchKernelGGL((frame_outer_kernel<T_, M_, 0, 8>), g, b, lds, s, a);                        \
+  if (C > 8) hipLaunchKernelGGL((frame_outer_kernel<T_, M_, 0, 16>), g, b, lds, s, a);                       \
+  else if (C > 4) hipLaunchKernelGGL((frame_outer_kernel<T_, M_, 0, 8>), g, b, lds, s, a);                   \
   else if (a.L == 20) hipLaunchKernelGGL((frame_outer_kernel<T_, M_, 20>), g, b, lds, s, a);                  \
   else if (a.L == 16) hipLaunchKernelGGL((frame_outer_kernel<T_, M_, 16>), g, b, lds, s, a);                  \
   else hipLaunchKernelGGL((frame_outer_kernel<T_, M_, 0>), g, b, lds, s, a);
@@ -857,6 +860,9 @@ hipError_t launch_dec_fwd(DType dt, const CodecArgs& a, hipStream_t s) {
     }
     if (a.N == 256) { CTN_DFM(8) } else { CTN_DFM(16) }
 #undef CTN_DFM
+  } else if (a.C > 8) {
+    if (dt == BF16) hipLaunchKernelGGL((dec_fwd_kernel<bf16raw, 16>), g, b, lds, s, a, rpb);
+    else hipLaunchKernelGGL((dec_fwd_kernel<float, 16>), g, b, lds, s, a, rpb);
   } else if (a.C > 4) {
     if (dt == BF16) hipLaunchKernelGGL((dec_fwd_kernel<bf16raw, 8>), g, b, lds, s, a, rpb);
     else hipLaunchKernelGGL((dec_fwd_kernel<float, 8>), g, b, lds, s, a, rpb);
@@ -907,6 +913,9 @@ hipError_t launch_dec_bwd(DType dt, const CodecArgs& a, hipStream_t s) {
     }
     if (a.N == 256) { CTN_DBM(16) } else { CTN_DBM(32) }
 #undef CTN_DBM
+  } else if (a.C > 8) {
+    if (dt == BF16) hipLaunchKernelGGL((dec_bwd_kernel<bf16raw, 16>), g, b, lds, s, a, rpb);
+    else hipLaunchKernelGGL((dec_bwd_kernel<float, 16>), g, b, lds, s, a, rpb);
   } else if (a.C > 4) {
     if (dt == BF16) hipLaunchKernelGGL((dec_bwd_kernel<bf16raw, 8>), g, b, lds, s, a, rpb);
     else hipLaunchKernelGGL((dec_bwd_kernel<float, 8>), g, b, lds, s, a, rpb);

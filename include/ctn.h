@@ -211,7 +211,8 @@ int ctn_decoder_backward(const ctn_codec_desc* d, const void* x_last, const void
  * permutations (:66) and keeps the first maximum (torch.argmax); 11 <= C <= 16, past what
  * the reference's C!-row one-hot table can hold, solves the same maximum as a linear
  * assignment (Hungarian, fp64) and reports its lexicographic rank in best_perm (exact ties
- * may pick another optimal permutation).  The encoder/decoder descriptors accept 1..8.
+ * may pick another optimal permutation).  The encoder/decoder descriptors accept 1..16
+ * (streaming: 1..8).
  * ------------------------------------------------------------------------- */
 typedef struct { int32_t M, C, T; } ctn_pit_desc;
 size_t ctn_pit_workspace_bytes(const ctn_pit_desc* d);

@@ -337,7 +337,8 @@ def si_snr_pit(source, est, lengths):
     ratio = (proj ** 2).sum(3) / ((noise ** 2).sum(3) + EPS)
     snr = 10 * torch.log10(ratio + EPS)                        # [B, C, C]
     perms = torch.tensor(list(itertools.permutations(range(C))), dtype=torch.long)
-    snr_set = torch.stack([snr[:, torch.arange(C), p].sum(1) for p in perms], 1)
+    # snr_set[b, p] = sum_i snr[b, i, perms[p, i]] (pit_criterion.py:66-71), one gather
+    snr_set = snr[:, torch.arange(C).view(1, C), perms].sum(2)
     idx = torch.argmax(snr_set, dim=1)
     max_snr = snr_set.max(dim=1, keepdim=True)[0] / C
     return max_snr, perms, idx, est

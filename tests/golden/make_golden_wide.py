@@ -6,6 +6,7 @@ Run from the repo root:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_gold
 pit_wide.npz   : cal_loss (pit_criterion.py:12-113) for C = 5, 6, 8 — C! = 120, 720,
                  40,320 permutations (pit_criterion.py:66) — equal and unequal lengths
 pit_c9_10.npz  : the same at C = 9 and 10 (python tests/golden/make_golden_wide.py --c9)
+model_9spk.npz : a full ConvTasNet forward + PIT loss + backward at C = 9 (small dims, --c9)
 model_5spk.npz : a full ConvTasNet forward + PIT loss + backward at C = 5 (small dims)
 """
 import numpy as np
@@ -73,10 +74,19 @@ def pit_c9_c10_fixtures():
 if __name__ == "__main__":
     import sys
     torch.manual_seed(0)
-    if "--c9" in sys.argv:   # only the C = 9, 10 fixtures (round 5)
+    if "--c9" in sys.argv:   # only the round-5 fixtures (C = 9, 10 PIT; the C = 9 model)
         pit_c9_c10_fixtures()
+        model_9spk()
         sys.exit(0)
     pit_wide_fixtures()
     pit_c9_c10_fixtures()
     mg.model_fixture("model_5spk.npz", O.Cfg(64, 20, 64, 128, 3, 2, 2, 5), 2, 4000, 6,
                      lens=[4000, 3300], full=True)
+    model_9spk()
+
+
+def model_9spk():
+    """model_9spk.npz (round 5): the full model at C = 9 (mask and decoder kernels with 16
+    speakers per row, PIT over 362,880 permutations), small dims"""
+    mg.model_fixture("model_9spk.npz", O.Cfg(32, 20, 32, 64, 3, 2, 1, 9), 2, 2000, 8,
+                     lens=[2000, 1500], full=True)

@@ -59,7 +59,7 @@ def run(model, g, bf16=False):
 
 
 MODELS = ["model_c1.npz", "model_paper_short.npz", "model_causal_cln.npz", "model_3spk.npz",
-          "model_softmax_pad.npz", "model_bn.npz", "model_5spk.npz"]
+          "model_softmax_pad.npz", "model_bn.npz", "model_5spk.npz", "model_9spk.npz"]
 
 
 @pytest.mark.parametrize("name", MODELS)
