@@ -17,8 +17,10 @@ raises ``CtnLibraryError`` (there is no fallback).
 from __future__ import annotations
 
 import ctypes
+import operator
 from collections import OrderedDict
 
+import numpy as np
 import torch
 
 import ctn_lib as L
@@ -101,16 +103,47 @@ _F32 = torch.float32
 
 
 def _fast_ok(ts, dev) -> bool:
-    """The checks of _check_tensor for a list that was fully checked before under the same
-    data pointers and sizes: dtype and layout only.  Device pointers are unique across
-    devices (one address space), so equal pointers mean the same devices; a sparse tensor
-    has no data pointer to match."""
+    """The checks of _check_tensor for tensors of a list whose sizes and order were fully
+    checked before: device, dtype and layout (one Python loop; a sparse tensor has no data
+    pointer and fails the contiguity check)."""
     if dev.type != "cuda":
         return False
+    di = dev.index if dev.index is not None else torch.cuda.current_device()
     for t in ts:
-        if t.dtype is not _F32 or not t.is_contiguous():
+        if t.dtype is not _F32 or not t.is_contiguous() or t.get_device() != di:
             return False
     return True
+
+
+def _ptrs(ts) -> np.ndarray:
+    return np.fromiter(map(_data_ptr, ts), dtype=np.uint64, count=len(ts))
+
+
+def _table(cols, n: int, device) -> torch.Tensor:
+    """Segment table [n] x (param, grad, exp_avg, exp_avg_sq, numel) from pointer columns
+    (numpy uint64, or None for 0) -> device, async from pinned memory (torch's pinned
+    caching allocator keeps the staging block alive until the copy has run)."""
+    host = torch.empty(n * ctypes.sizeof(L.OptSegment), dtype=torch.uint8, pin_memory=True)
+    a = host.numpy().view(np.uint64).reshape(n, 5)
+    for i, c in enumerate(cols):
+        a[:, i] = 0 if c is None else c
+    return host.to(device, non_blocking=True)
+
+
+class _FastTable:
+    """The device segment table of the last call with these sizes: re-uploaded only when a
+    pointer column changed (the caching allocator may hand the gradients other blocks)."""
+
+    def __init__(self):
+        self.cols = None
+        self.dev_table = None
+
+    def get(self, cols, n, device):
+        if self.cols is None or any(a is None and b is not None or a is not None and (b is None or not np.array_equal(a, b))
+                                    for a, b in zip(cols, self.cols)):
+            self.dev_table = _table(cols, n, device)
+            self.cols = cols
+        return self.dev_table
 
 
 # fast-path hits and misses since import (host instrumentation, tools/exp/host_phases.py)
@@ -118,9 +151,11 @@ FAST_STATS = {"clip_hit": 0, "clip_miss": 0, "adam_hit": 0, "adam_miss": 0}
 
 
 # Host fast path (VERDICT r04 Next 6: clip and Adam spent ~1 ms of host time each per step
-# on per-tensor Python over 294 tensors).  A call whose gradient pointers and sizes equal a
-# previous fully checked call's reuses that call's device segment table and chunk plan;
-# anything else takes the full path.  Keyed by the pointer tuple, at most 8 entries.
+# on per-tensor Python over 294 tensors).  A call whose gradient sizes and 16-byte
+# alignments equal a previous fully checked call's reuses that call's chunk plan and builds
+# the pointer table with numpy (the gradients' pointers change from step to step when
+# zero_grad(set_to_none=True) frees them); anything else takes the full path.  At most 8
+# entries.
 _clip_fast: OrderedDict = OrderedDict()
 
 
@@ -138,11 +173,13 @@ def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0, error_i
     if float(norm_type) != 2.0:
         raise L.CtnLibraryError(f"clip_grad_norm_: norm_type {norm_type} is not implemented (2.0 only)")
     dev = grads[0].device
-    ptrs = tuple(map(_data_ptr, grads))
-    fast = _clip_fast.get(ptrs)
-    if fast is not None and fast[0] == tuple(map(_numel, grads)) and _fast_ok(grads, dev):
-        plan, segs_dev = fast[1], fast[2]
-        _clip_fast.move_to_end(ptrs)
+    n = len(grads)
+    gp = _ptrs(grads)
+    key = (dev, tuple(map(_numel, grads)), (gp % 16 == 0).tobytes())
+    fast = _clip_fast.get(key)
+    if fast is not None and _fast_ok(grads, dev):
+        plan, tab = fast
+        _clip_fast.move_to_end(key)
         FAST_STATS["clip_hit"] += 1
     else:
         FAST_STATS["clip_miss"] += 1
@@ -151,12 +188,13 @@ def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0, error_i
             if g.device != dev:
                 raise L.CtnLibraryError("clip_grad_norm_: gradients on more than one device")
         segs = [L.OptSegment(None, g.data_ptr(), None, None, g.numel()) for g in grads]
-        key = (dev, tuple((g.numel(), _aligned(g)) for g in grads))
-        plan = _cached_plan(_clip_plans, key, lambda: _Plan(segs, dev))
-        segs_dev = plan.segments(segs, ptrs)
-        _clip_fast[ptrs] = (tuple(map(_numel, grads)), plan, segs_dev)
+        plan = _cached_plan(_clip_plans, (dev, tuple((g.numel(), _aligned(g)) for g in grads)),
+                            lambda: _Plan(segs, dev))
+        tab = _FastTable()
+        _clip_fast[key] = (plan, tab)
         while len(_clip_fast) > _PLAN_CACHE_MAX:
             _clip_fast.popitem(last=False)
+    segs_dev = tab.get((None, gp, None, None, np.array(key[1], dtype=np.uint64)), n, dev)
     total = torch.empty((), dtype=torch.float32, device=dev)
     L.check(L.load().ctn_grad_clip_norm(segs_dev.data_ptr(), plan.chunks.data_ptr(), plan.nchunks,
                                         float(max_norm), total.data_ptr(), plan.partial.data_ptr(),
@@ -197,7 +235,7 @@ class Adam(torch.optim.Optimizer):
             if f is not None and f[4]:
                 for p, _, _, _ in f[0]:
                     self._steps[p] = f[3]
-                self._fast[gi] = f[:4] + (False,)
+                self._fast[gi] = f[:4] + (False,) + f[5:]
 
     # --- state_dict compatibility: keep state['step'] tensors current
     def _sync_steps(self):
@@ -269,32 +307,40 @@ class Adam(torch.optim.Optimizer):
                 # checks; derived weight copies such as ctn_ops.WeightPacks)
                 _bump([it[0] for it in items])
                 if len(by_step) == 1:   # one step count: the next call may take the fast path
-                    self._fast[gi] = (items, plan, segs_dev, n, False,
-                                      self._fast_key(items[0][0].device, [it[0] for it in items]))
+                    ps, gs = [it[0] for it in items], [it[1] for it in items]
+                    ms, vs = [it[2] for it in items], [it[3] for it in items]
+                    cols = (_ptrs(ms), _ptrs(vs), np.fromiter((p.numel() for p in ps), np.uint64, len(items)))
+                    self._fast[gi] = (items, plan, _FastTable(), n, False,
+                                      self._fast_key(ps[0].device, gs, (_ptrs(ps), _ptrs(gs), cols[0], cols[1])),
+                                      cols)
             if len(by_step) != 1:
                 self._fast[gi] = None
         return loss
 
     @staticmethod
-    def _fast_key(dev, params):
-        grads = [p.grad for p in params]
-        return (dev, tuple(map(_data_ptr, params)), tuple(map(_data_ptr, grads)), tuple(map(_numel, grads)))
+    def _fast_key(dev, grads, pcols):
+        """sizes and the 16-byte alignment of every (param, grad, exp_avg, exp_avg_sq) row:
+        the chunk plan's inputs (ctn_opt_plan)"""
+        al = pcols[0] | pcols[1] | pcols[2] | pcols[3]
+        return (dev, tuple(map(_numel, grads)), (al % 16 == 0).tobytes())
 
     def _fast_step(self, lib, gi, group) -> bool:
-        """The step of a group whose parameters, gradients and states are those of its last
-        fully checked call (same objects, pointers and sizes, one step count): reuse that
-        call's segment table and plan; the per-parameter bookkeeping is folded in lazily
+        """The step of a group whose parameters and states are those of its last fully
+        checked call (same objects, one step count) and whose gradients have the same sizes
+        and alignments: reuse that call's plan and state pointer columns, take the
+        gradient pointers with numpy; the per-parameter bookkeeping is folded in lazily
         (_flush_fast)."""
         f = self._fast.get(gi)
         if f is None:
             return False
-        items, plan, segs_dev, n, _, key = f
+        items, plan, tab, n, _, key, cols = f
         params = [p for p in group["params"] if p.grad is not None]
-        if len(params) != len(items) or any(p is not it[0] for p, it in zip(params, items)):
+        if len(params) != len(items) or not all(map(operator.is_, params, [it[0] for it in items])):
             return False
         dev = items[0][0].device
         grads = [p.grad for p in params]
-        if self._fast_key(dev, params) != key or not _fast_ok(grads, dev):
+        pp, gp = _ptrs(params), _ptrs(grads)
+        if self._fast_key(dev, grads, (pp, gp, cols[0], cols[1])) != key or not _fast_ok(grads, dev):
             return False
         state = self.state
         for p, it in zip(params, items):   # state tensors replaced (e.g. by the user)
@@ -305,8 +351,9 @@ class Adam(torch.optim.Optimizer):
         b1, b2 = group["betas"]
         hp = L.AdamHParams(float(group["lr"]), float(b1), float(b2), float(group["eps"]),
                            float(group["weight_decay"]), n)
+        segs_dev = tab.get((pp, gp, cols[0], cols[1], cols[2]), len(params), dev)
         L.check(lib.ctn_adam_step(segs_dev.data_ptr(), plan.chunks.data_ptr(), plan.nchunks,
                                   ctypes.byref(hp), L.stream_handle(dev)), "ctn_adam_step")
         _bump(params)
-        self._fast[gi] = (items, plan, segs_dev, n, True, key)
+        self._fast[gi] = (items, plan, tab, n, True, key, cols)
         return True

@@ -200,3 +200,30 @@ def test_fast_paths_match_torch():
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
     sd = o_hip.state_dict()
     assert [float(sd["state"][i]["step"]) for i in range(3)] == [7.0, 6.0, 7.0]
+
+
+@pytest.mark.gpu
+def test_fast_paths_with_fresh_gradients_each_step():
+    """zero_grad(set_to_none=True) training: every step's gradients are new tensors at
+    other addresses (a spacer allocation shifts them); the fast paths still apply (same
+    sizes and alignments) with the pointer table rebuilt, and the updates equal torch's."""
+    import ctn_optim
+    dev = torch.device("cuda")
+    ps = [torch.nn.Parameter(t) for t in _params(dev)]
+    qs = [torch.nn.Parameter(t.clone()) for t in _params(dev)]
+    o_hip = ctn_optim.Adam(ps, lr=1e-3)
+    o_ref = torch.optim.Adam(qs, lr=1e-3, foreach=False)
+    hits0 = dict(ctn_optim.FAST_STATS)
+    keep = []
+    for step in range(6):
+        keep.append(torch.empty(1000 * (step + 1), device=dev))     # moves the next allocations
+        for a, b, g in zip(ps, qs, _grads(ps, 80 + step)):
+            a.grad, b.grad = g.clone(), g.clone()
+        torch.testing.assert_close(ctn_optim.clip_grad_norm_(ps, 1.0), torch.nn.utils.clip_grad_norm_(qs, 1.0),
+                                   rtol=1e-6, atol=0)
+        o_hip.step()
+        o_ref.step()
+        for a, b in zip(ps, qs):
+            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+    assert ctn_optim.FAST_STATS["clip_hit"] - hits0["clip_hit"] >= 4
+    assert ctn_optim.FAST_STATS["adam_hit"] - hits0["adam_hit"] >= 4

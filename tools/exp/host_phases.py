@@ -75,3 +75,13 @@ for x in w:
         print("SYNC:", k)
 print(f"{len(w)} sync warnings in 2 steps")
 print("optimizer fast paths:", ctn_optim.FAST_STATS, "(sync mode)" if SYNC else "")
+if "--cprofile" in sys.argv:   # where the host time of 5 steps goes, by function
+    import cProfile
+    import pstats
+    pr = cProfile.Profile()
+    pr.enable()
+    for _ in range(5):
+        step(False)
+    pr.disable()
+    torch.cuda.synchronize()
+    pstats.Stats(pr).sort_stats("tottime").print_stats(30)
