@@ -297,6 +297,9 @@ def main():
     ap.add_argument("--ddp", action="store_true",
                     help="the data-parallel path over RCCL even at world size 1 (process-group init, "
                          "gradient exchange)")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture the whole step as a HIP graph after warmup and time its replays "
+                         "(ctn_graph.StepGraph; one GPU, no exchange)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -375,10 +378,12 @@ def main():
             static_graph=os.environ.get("CTN_DDP_STATIC", "1") == "1")
     # the solver's update (src/solver.py:184-186) on the HIP path: one launch for
     # the clip norm, one for the clip scale, one for Adam over all 294 tensors
-    opt = ctn_optim.Adam(model.parameters(), lr=1e-3)
+    opt = ctn_optim.Adam(model.parameters(), lr=1e-3, capturable=args.graph)
     mix, src = synthetic.speech_like(M, C, T, 1234 + rank)
     mix, src = mix.to(dev), src.to(dev)
     lens = torch.full((M,), T, dtype=torch.int64, device=dev)
+
+    plist = list(model.parameters())   # (model.parameters() walks every module each call)
 
     def step():
         est = model(mix)
@@ -387,7 +392,7 @@ def main():
         loss.backward()
         if grad_sync is not None:
             grad_sync.sync()
-        ctn_optim.clip_grad_norm_(model.parameters(), 5.0)
+        ctn_optim.clip_grad_norm_(plist, 5.0)
         opt.step()
         return loss
 
@@ -420,14 +425,21 @@ def main():
     if not args.timer_kind:   # the kernel family with the most time per step
         args.timer_kind = max(table, key=lambda k: table[k]["ms_per_step"]) if table else TIMER_GEMM_BWD_A
     n_def0 = ctn_ops.DEFERRED_BLOCKS
+    graph = None
+    if args.graph:
+        if use_ddp:
+            sys.exit("bench.py: --graph runs one process on one GPU (no exchange inside the graph)")
+        import ctn_graph
+        graph = ctn_graph.StepGraph(step, warmup=1)   # one more eager step on a side stream, then capture
     torch.cuda.synchronize(dev)
-    L.check(lib.ctn_timer_enable(args.timer_kind, args.steps * 64), "ctn_timer_enable")
+    if graph is None:   # (a replay re-runs the captured launches: the live timer sees none of them)
+        L.check(lib.ctn_timer_enable(args.timer_kind, args.steps * 64), "ctn_timer_enable")
     if use_ddp:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = step()
+        loss = step() if graph is None else graph.replay()
     torch.cuda.synchronize(dev)
     if use_ddp:
         dist.barrier()
@@ -457,6 +469,9 @@ def main():
         utt_s = world * M * args.steps / elapsed
         kb = kernel_bytes(args.timer_kind, M, K, cfg, s)
         mean_ms = tot.value / max(nl.value, 1)
+        if graph is not None and args.timer_kind in table:   # graph: the eager profile pass's timing
+            mean_ms = table[args.timer_kind]["mean_us"] * 1e-3
+            nl.value = int(round(table[args.timer_kind]["launches_per_step"] * args.steps))
         achieved = kb / (mean_ms * 1e-3) / 1e9
         traffic = mfma = step_pmc = None
         pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")   # c2 FETCH_SIZE/WRITE_SIZE passes
@@ -498,6 +513,8 @@ def main():
                                       + (" REHEARSAL: all ranks on one GPU over gloo" if _rehearsal() else ""),
                        "rccl_world_size": dist.get_world_size() if use_ddp and not _rehearsal() else None,
                        "rank_ms_per_step": rank_ms,
+                       # timed steps as replays of one captured HIP graph (--graph)
+                       "hip_graph": graph is not None,
                        # TemporalBlock backwards per step whose parameter-gradient reductions
                        # ran batched at the end of backward (ctn_tblock_reduce_grads)
                        "deferred_grad_reduce_blocks": deferred},

@@ -284,11 +284,25 @@ class TemporalBlock(nn.Module):
         return (m['0'].weight, m['1'].weight, g1, b1, ds['0'].weight,
                 ds[str(1 + off)].weight, g2, b2, ds[str(3 + off)].weight)
 
+    def _acc_nodes(self, params):
+        """The parameters' AccumulateGrad nodes (what ctn_ops reads to decide whether a late
+        gradient write is unobservable), held by this module: the same node objects every
+        step (autograd keeps a leaf's accumulator while anyone holds it), found once instead
+        of per forward; recomputed when a parameter was replaced."""
+        c = getattr(self, "_acc_cache", None)
+        if c is None or len(c[0]) != len(params) or any(a is not b for a, b in zip(c[0], params)):
+            nodes = tuple(torch.autograd.graph.get_gradient_edge(t).node if t.requires_grad and t.is_leaf else None
+                          for t in params)
+            object.__setattr__(self, "_acc_cache", c := (tuple(params), nodes))
+        return c[1]
+
     def _forward_rows(self, x_rows, fr, norm, pack=None, wgrad_split=False, defer=False):
         B, H, P, dil, causal, _ = self._geo
         bn = ops.bn_state(*self._norms()) if norm == L.NORM_BN else None
-        return ops.TBlockFn.apply(x_rows, fr, (B, H, P, dil, causal, norm, wgrad_split, defer), pack, bn,
-                                  *self._params())
+        params = self._params()
+        nodes = self._acc_nodes(params) if (wgrad_split or defer) and torch.is_grad_enabled() else None
+        return ops.TBlockFn.apply(x_rows, fr, (B, H, P, dil, causal, norm, wgrad_split, defer, nodes), pack, bn,
+                                  *params)
 
     def forward(self, x):
         """x [M, B, K] -> [M, B, K]."""

@@ -154,9 +154,13 @@ int dev_err_slot(int* dev) {
 }
 
 const char* dev_err_text(uint32_t w) {
-  return (w & CTN_DEVERR_SPIN) ? "a generation-word wait of a wave-specialised kernel ran out of polls "
-                                      "(CTN_DEVERR_SPIN): that launch's outputs are invalid"
-                                    : "unknown device error bit";
+  if (w & CTN_DEVERR_SPIN)
+    return "a generation-word wait of a wave-specialised kernel ran out of polls (CTN_DEVERR_SPIN): that launch's "
+           "outputs are invalid";
+  if (w & CTN_DEVERR_ADAM_TABLE)
+    return "ctn_adam_step_dev ran past its bias-correction table (CTN_DEVERR_ADAM_TABLE): the parameters were not "
+           "updated";
+  return "unknown device error bit";
 }
 
 // the mirror of earlier copies (no synchronisation): non-zero once an error has been seen
@@ -1536,6 +1540,36 @@ extern "C" int ctn_adam_step(const ctn_opt_segment* segs, const ctn_opt_chunk* c
   AdamArgs a{hp->beta1, hp->beta2, hp->eps, hp->weight_decay, (float)(hp->lr / bc1), (float)sqrt(bc2)};
   CTN_HIP(launch_adam(reinterpret_cast<const OptSegment*>(segs), reinterpret_cast<const OptChunk*>(chunks), nchunks,
                       a, (hipStream_t)stream));
+  return CTN_OK;
+}
+
+extern "C" int ctn_opt_write_segments(ctn_opt_segment* dst, const ctn_opt_segment* src, int n, void* stream) {
+  if (!dst || n < 0 || (n > 0 && !src)) return fail(CTN_ERR_ARG, "ctn_opt_write_segments: bad arguments");
+  CTN_HIP(launch_write_segments(reinterpret_cast<OptSegment*>(dst), reinterpret_cast<const OptSegment*>(src), n,
+                                (hipStream_t)stream));
+  return CTN_OK;
+}
+
+extern "C" int ctn_adam_table(const ctn_adam_hparams* hp, int32_t count, float* table) {
+  if (!hp || count < 0 || (count > 0 && !table)) return fail(CTN_ERR_ARG, "ctn_adam_table: bad arguments");
+  for (int32_t i = 0; i < count; ++i) {   // ctn_adam_step's arithmetic for step i + 1
+    const double bc1 = 1.0 - pow((double)hp->beta1, (double)(i + 1));
+    const double bc2 = 1.0 - pow((double)hp->beta2, (double)(i + 1));
+    table[2 * i] = (float)(hp->lr / bc1);
+    table[2 * i + 1] = (float)sqrt(bc2);
+  }
+  return CTN_OK;
+}
+
+extern "C" int ctn_adam_step_dev(const ctn_opt_segment* segs, const ctn_opt_chunk* chunks, int nchunks,
+                                 const ctn_adam_hparams* hp, const float* table_dev, int32_t table_len,
+                                 int32_t* counter, void* stream) {
+  if (!segs || !chunks || !hp || nchunks < 0 || !table_dev || table_len < 1 || !counter)
+    return fail(CTN_ERR_ARG, "ctn_adam_step_dev: bad arguments");
+  AdamArgs a{hp->beta1, hp->beta2, hp->eps, hp->weight_decay, 0.f, 1.f};
+  CTN_HIP(launch_adam_dev(reinterpret_cast<const OptSegment*>(segs), reinterpret_cast<const OptChunk*>(chunks),
+                          nchunks, a, reinterpret_cast<const float2*>(table_dev), table_len, counter,
+                          ctn::device_error_word(), (hipStream_t)stream));
   return CTN_OK;
 }
 

@@ -315,6 +315,9 @@ hipError_t launch_grad_clip(const OptSegment* segs, const OptChunk* chunks, int 
                             float max_norm, float* total_norm, hipStream_t s);
 hipError_t launch_adam(const OptSegment* segs, const OptChunk* chunks, int nchunks, const AdamArgs& a,
                        hipStream_t s);
+hipError_t launch_adam_dev(const OptSegment* segs, const OptChunk* chunks, int nchunks, const AdamArgs& a,
+                           const float2* table, int table_len, int* counter, uint32_t* err, hipStream_t s);
+hipError_t launch_write_segments(OptSegment* dst, const OptSegment* src, int n, hipStream_t s);
 
 // ---- streaming causal separation (ctn_stream.hip) ----------------------------------
 struct StreamArgs {

@@ -125,6 +125,86 @@ __global__ __launch_bounds__(OPT_THREADS) void adam_kernel(const OptSegment* seg
   for (int i = done + threadIdx.x; i < len; i += OPT_THREADS) adam_elem(p[i], g[i], m[i], v[i], a);
 }
 
+// Graph-capturable Adam (ABI v10): the step count lives in device memory and the bias
+// corrections of step t come from a host-computed table (the same double arithmetic as
+// ctn_adam_step, so the same bits), so a captured step replays correctly; a bump kernel
+// advances the count after the update.  t past the table sets CTN_DEVERR_ADAM_TABLE and
+// leaves the parameters untouched.
+__global__ __launch_bounds__(OPT_THREADS) void adam_dev_kernel(const OptSegment* segs, const OptChunk* chunks,
+                                                               AdamArgs a, const float2* table, int table_len,
+                                                               const int* counter, uint32_t* err) {
+  const int t = *counter + 1;
+  if (t < 1 || t > table_len) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && err) atomicOr(err, (uint32_t)CTN_DEVERR_ADAM_TABLE);
+    return;
+  }
+  const float2 bc = table[t - 1];
+  a.step_size = bc.x;
+  a.bc2_sqrt = bc.y;
+  int si, len; long off; bool vec;
+  opt_chunk(chunks, si, off, len, vec);
+  const OptSegment s = segs[si];
+  float* p = s.p + off;
+  const float* g = s.g + off;
+  float* m = s.m + off;
+  float* v = s.v + off;
+  int done = 0;
+  if (vec) {
+    const int n4 = len >> 2;
+    for (int i = threadIdx.x; i < n4; i += OPT_THREADS) {
+      float4 P = reinterpret_cast<float4*>(p)[i];
+      const float4 G = reinterpret_cast<const float4*>(g)[i];
+      float4 Mv = reinterpret_cast<float4*>(m)[i];
+      float4 V = reinterpret_cast<float4*>(v)[i];
+      adam_elem(P.x, G.x, Mv.x, V.x, a);
+      adam_elem(P.y, G.y, Mv.y, V.y, a);
+      adam_elem(P.z, G.z, Mv.z, V.z, a);
+      adam_elem(P.w, G.w, Mv.w, V.w, a);
+      reinterpret_cast<float4*>(p)[i] = P;
+      reinterpret_cast<float4*>(m)[i] = Mv;
+      reinterpret_cast<float4*>(v)[i] = V;
+    }
+    done = n4 << 2;
+  }
+  for (int i = done + threadIdx.x; i < len; i += OPT_THREADS) adam_elem(p[i], g[i], m[i], v[i], a);
+}
+
+__global__ void adam_bump_kernel(int* counter) {
+  if (threadIdx.x == 0) *counter += 1;   // vector store: one lane of one wave
+}
+
+// Segment tables written by kernels whose arguments carry the entries (captured into a
+// graph with the values of the capture, no host staging buffer): OPT_SEG_BATCH per launch
+constexpr int OPT_SEG_BATCH = 64;
+struct SegBatch { OptSegment e[OPT_SEG_BATCH]; int n; };
+__global__ void write_segments_kernel(OptSegment* dst, SegBatch b) {
+  const int i = threadIdx.x;
+  if (i < b.n) dst[i] = b.e[i];
+}
+
+hipError_t launch_write_segments(OptSegment* dst, const OptSegment* src, int n, hipStream_t s) {
+  if (!dst || (n > 0 && !src) || n < 0) return hipErrorInvalidValue;
+  for (int i0 = 0; i0 < n; i0 += OPT_SEG_BATCH) {
+    SegBatch b{};
+    b.n = n - i0 < OPT_SEG_BATCH ? n - i0 : OPT_SEG_BATCH;
+    for (int i = 0; i < b.n; ++i) b.e[i] = src[i0 + i];
+    hipLaunchKernelGGL(write_segments_kernel, dim3(1), dim3(OPT_SEG_BATCH), 0, s, dst + i0, b);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+hipError_t launch_adam_dev(const OptSegment* segs, const OptChunk* chunks, int nchunks, const AdamArgs& a,
+                           const float2* table, int table_len, int* counter, uint32_t* err, hipStream_t s) {
+  if (!segs || !chunks || nchunks < 0 || !table || table_len < 1 || !counter) return hipErrorInvalidValue;
+  if (nchunks > 0)
+    hipLaunchKernelGGL(adam_dev_kernel, dim3(nchunks), dim3(OPT_THREADS), 0, s, segs, chunks, a, table, table_len,
+                       counter, err);
+  hipLaunchKernelGGL(adam_bump_kernel, dim3(1), dim3(64), 0, s, counter);
+  return hipGetLastError();
+}
+
 static hipError_t opt_check(const OptSegment* segs, const OptChunk* chunks, int nchunks) {
   if (!segs || !chunks || nchunks < 0) return hipErrorInvalidValue;
   return hipSuccess;

@@ -356,14 +356,18 @@ class TBlockFn(torch.autograd.Function):
         parameter-gradient tail on a second stream when that is unobservable (_split_ok).
         cfg[7] (optional, ConvTasNet.defer_grad_reduce): leave the parameter-gradient
         reductions to one batched call at the end of the backward pass when that is
-        unobservable (_grads_unobserved; not with the side stream)."""
+        unobservable (_grads_unobserved; not with the side stream).
+        cfg[8] (optional): the parameters' AccumulateGrad nodes, cached by the caller."""
         B, H, P, dil, causal, norm = cfg[:6]
         ctx.wgrad_split = len(cfg) > 6 and bool(cfg[6])
         ctx.defer = len(cfg) > 7 and bool(cfg[7]) and norm != L.NORM_BN
         if ctx.wgrad_split or ctx.defer:
             ctx.param_refs = (w1, a1, g1, b1, wd, a2, g2, b2, w2)
-            ctx.acc_nodes = tuple(torch.autograd.graph.get_gradient_edge(t).node if t.requires_grad and t.is_leaf
-                                  else None for t in ctx.param_refs)
+            # cfg[8]: the nodes cached by the module (conv_tasnet.TemporalBlock._acc_nodes)
+            nodes = cfg[8] if len(cfg) > 8 else None
+            ctx.acc_nodes = nodes if nodes is not None else tuple(
+                torch.autograd.graph.get_gradient_edge(t).node if t.requires_grad and t.is_leaf else None
+                for t in ctx.param_refs)
             _register_uses(ctx, ctx.param_refs)
         lib = L.load()
         L.require_device(x, "TemporalBlock")

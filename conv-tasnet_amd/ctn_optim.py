@@ -64,13 +64,18 @@ class _Plan:
 
 
 def upload_segments(segs: list, device) -> torch.Tensor:
-    """Segment table -> device, async: torch's pinned-host caching allocator keeps
-    the staging block alive until the copy has run, so no later call can
-    overwrite it while the CPU runs ahead of the GPU."""
+    """Segment table -> device by kernels whose arguments carry the entries
+    (ctn_opt_write_segments): stream-ordered, no host staging buffer to keep alive, and
+    capturable into a graph with the values of the capture."""
     arr = (L.OptSegment * len(segs))(*segs)
-    host = torch.empty(ctypes.sizeof(arr), dtype=torch.uint8, pin_memory=True)
-    ctypes.memmove(host.data_ptr(), ctypes.addressof(arr), ctypes.sizeof(arr))
-    return host.to(device, non_blocking=True)
+    return _write_table(ctypes.addressof(arr), len(segs), device)
+
+
+def _write_table(host_addr: int, n: int, device) -> torch.Tensor:
+    dst = torch.empty(max(n, 1) * ctypes.sizeof(L.OptSegment), dtype=torch.uint8, device=device)
+    L.check(L.load().ctn_opt_write_segments(dst.data_ptr(), host_addr, n, L.stream_handle(device)),
+            "ctn_opt_write_segments")
+    return dst
 
 
 def _aligned(*ts) -> bool:
@@ -121,13 +126,12 @@ def _ptrs(ts) -> np.ndarray:
 
 def _table(cols, n: int, device) -> torch.Tensor:
     """Segment table [n] x (param, grad, exp_avg, exp_avg_sq, numel) from pointer columns
-    (numpy uint64, or None for 0) -> device, async from pinned memory (torch's pinned
-    caching allocator keeps the staging block alive until the copy has run)."""
-    host = torch.empty(n * ctypes.sizeof(L.OptSegment), dtype=torch.uint8, pin_memory=True)
-    a = host.numpy().view(np.uint64).reshape(n, 5)
+    (numpy uint64, or None for 0) -> device (_write_table)."""
+    a = np.zeros((n, 5), dtype=np.uint64)
     for i, c in enumerate(cols):
-        a[:, i] = 0 if c is None else c
-    return host.to(device, non_blocking=True)
+        if c is not None:
+            a[:, i] = c
+    return _write_table(a.ctypes.data, n, device)
 
 
 class _FastTable:
@@ -213,7 +217,8 @@ class Adam(torch.optim.Optimizer):
     Adam), ``exp_avg`` and ``exp_avg_sq`` (device tensors shaped like ``p``)."""
 
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 0.0, amsgrad: bool = False, *, maximize: bool = False, **_ignored):
+                 weight_decay: float = 0.0, amsgrad: bool = False, *, maximize: bool = False,
+                 capturable: bool = False, **_ignored):
         if amsgrad or maximize:
             raise L.CtnLibraryError("Adam: amsgrad / maximize are not implemented on the HIP path")
         if not 0.0 <= lr or not 0.0 <= eps or not 0.0 <= weight_decay:
@@ -221,8 +226,11 @@ class Adam(torch.optim.Optimizer):
         if not (0.0 <= betas[0] < 1.0 and 0.0 <= betas[1] < 1.0):
             raise ValueError(f"Adam: invalid betas {betas}")
         defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay, amsgrad=False,
-                        maximize=False, foreach=None, capturable=False, differentiable=False, fused=None)
+                        maximize=False, foreach=None, capturable=bool(capturable), differentiable=False,
+                        fused=None)
         super().__init__(params, defaults)
+        # capturable groups: device step counter and bias-correction table per group
+        self._cap: dict = {}
         self._plans: OrderedDict = OrderedDict()
         self._steps: dict = {}   # param -> int step (mirrored into state['step'] lazily)
         # per param group: the last fully checked call whose parameters all had one step
@@ -237,9 +245,77 @@ class Adam(torch.optim.Optimizer):
                     self._steps[p] = f[3]
                 self._fast[gi] = f[:4] + (False,) + f[5:]
 
+    # --- graph capture (torch.optim.Adam(capturable=True) semantics): the step count of a
+    # capturable group lives in a device counter that the update kernel reads and a second
+    # kernel advances, and the bias corrections come from a device table built for the
+    # group's lr and betas (ctn_adam_table: ctn_adam_step's arithmetic, the same bits), so a
+    # captured step replays with the right step count.
+    TABLE_STEPS = 1 << 20
+
+    def _capture_state(self, gi, group, dev, completed: int):
+        c = self._cap.get(gi)
+        if c is None:
+            c = self._cap[gi] = {"counter": torch.full((1,), completed, dtype=torch.int32, device=dev),
+                                 "table": torch.empty(2 * self.TABLE_STEPS, dtype=torch.float32, device=dev),
+                                 "key": None}
+        b1, b2 = group["betas"]
+        key = (float(group["lr"]), float(b1), float(b2))
+        if c["key"] != key:
+            if torch.cuda.is_current_stream_capturing():
+                raise L.CtnLibraryError("Adam(capturable=True): lr or betas changed inside a graph capture; "
+                                        "step once eagerly after changing them, then capture")
+            host = np.empty(2 * self.TABLE_STEPS, dtype=np.float32)
+            hp = L.AdamHParams(key[0], key[1], key[2], 0.0, 0.0, 1)
+            L.check(L.load().ctn_adam_table(ctypes.byref(hp), self.TABLE_STEPS, host.ctypes.data), "ctn_adam_table")
+            c["table"].copy_(torch.from_numpy(host))
+            c["key"] = key
+        return c
+
+    def _launch(self, lib, gi, group, dev, segs_dev, plan, n: int):
+        """Step n (1-based) of a group: ctn_adam_step, or for a capturable group
+        ctn_adam_step_dev with the group's device counter (which must hold n - 1)."""
+        b1, b2 = group["betas"]
+        hp = L.AdamHParams(float(group["lr"]), float(b1), float(b2), float(group["eps"]),
+                           float(group["weight_decay"]), n)
+        if not group.get("capturable", False):
+            L.check(lib.ctn_adam_step(segs_dev.data_ptr(), plan.chunks.data_ptr(), plan.nchunks,
+                                      ctypes.byref(hp), L.stream_handle(dev)), "ctn_adam_step")
+            return
+        c = self._capture_state(gi, group, dev, n - 1)
+        L.check(lib.ctn_adam_step_dev(segs_dev.data_ptr(), plan.chunks.data_ptr(), plan.nchunks, ctypes.byref(hp),
+                                      c["table"].data_ptr(), self.TABLE_STEPS, c["counter"].data_ptr(),
+                                      L.stream_handle(dev)), "ctn_adam_step_dev")
+
+    def zero_grad(self, set_to_none: bool = True):
+        """torch.optim.Optimizer.zero_grad without its per-call profiler scope and
+        per-parameter foreach grouping: set_to_none drops every .grad (one Python loop);
+        otherwise the gradients are zeroed in place (detached first if they carry a graph,
+        as torch does)."""
+        for group in self.param_groups:
+            for p in group["params"]:
+                g = p.grad
+                if g is None:
+                    continue
+                if set_to_none:
+                    p.grad = None
+                else:
+                    if g.grad_fn is not None:
+                        g.detach_()
+                    else:
+                        g.requires_grad_(False)
+                    g.zero_()
+
     # --- state_dict compatibility: keep state['step'] tensors current
     def _sync_steps(self):
         self._flush_fast()
+        for gi, c in self._cap.items():   # capturable: the device counter is the truth (synchronises)
+            n = int(c["counter"].item())
+            for p in self.param_groups[gi]["params"]:
+                if p in self._steps:
+                    self._steps[p] = n
+            f = self._fast.get(gi)
+            if f is not None:
+                self._fast[gi] = f[:3] + (n,) + f[4:]
         for p, n in self._steps.items():
             st = self.state.get(p)
             if st is not None:
@@ -253,6 +329,7 @@ class Adam(torch.optim.Optimizer):
         super().load_state_dict(state_dict)
         self._steps = {}
         self._fast = {}
+        self._cap = {}
         for group in self.param_groups:
             for p in group["params"]:
                 st = self.state.get(p)
@@ -290,7 +367,8 @@ class Adam(torch.optim.Optimizer):
                 n = self._steps.get(p, int(float(st["step"]))) + 1
                 self._steps[p] = n
                 by_step.setdefault(n, []).append((p, g, st["exp_avg"], st["exp_avg_sq"]))
-            b1, b2 = group["betas"]
+            if group.get("capturable", False) and len(by_step) > 1:
+                raise L.CtnLibraryError("Adam(capturable=True): the parameters of a group need one step count")
             for n, items in by_step.items():
                 dev = items[0][0].device
                 segs = [L.OptSegment(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel())
@@ -298,10 +376,7 @@ class Adam(torch.optim.Optimizer):
                 key = (dev, tuple((p.numel(), _aligned(p, g, m, v)) for p, g, m, v in items))
                 plan = _cached_plan(self._plans, key, lambda: _Plan(segs, dev))
                 segs_dev = plan.segments(segs, tuple(t.data_ptr() for it in items for t in it))
-                hp = L.AdamHParams(float(group["lr"]), float(b1), float(b2), float(group["eps"]),
-                                   float(group["weight_decay"]), n)
-                L.check(lib.ctn_adam_step(segs_dev.data_ptr(), plan.chunks.data_ptr(), plan.nchunks,
-                                          ctypes.byref(hp), L.stream_handle(dev)), "ctn_adam_step")
+                self._launch(lib, gi, group, dev, segs_dev, plan, n)
                 # the kernel wrote through raw pointers: bump the parameters' version
                 # counters as an in-place torch update would (autograd's saved-tensor
                 # checks; derived weight copies such as ctn_ops.WeightPacks)
@@ -348,12 +423,8 @@ class Adam(torch.optim.Optimizer):
             if st["exp_avg"] is not it[2] or st["exp_avg_sq"] is not it[3]:
                 return False
         n += 1
-        b1, b2 = group["betas"]
-        hp = L.AdamHParams(float(group["lr"]), float(b1), float(b2), float(group["eps"]),
-                           float(group["weight_decay"]), n)
         segs_dev = tab.get((pp, gp, cols[0], cols[1], cols[2]), len(params), dev)
-        L.check(lib.ctn_adam_step(segs_dev.data_ptr(), plan.chunks.data_ptr(), plan.nchunks,
-                                  ctypes.byref(hp), L.stream_handle(dev)), "ctn_adam_step")
+        self._launch(lib, gi, group, dev, segs_dev, plan, n)
         _bump(params)
         self._fast[gi] = (items, plan, tab, n, True, key, cols)
         return True

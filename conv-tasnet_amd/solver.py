@@ -202,7 +202,8 @@ class Solver(object):
         if hasattr(getattr(loader, "sampler", None), "set_epoch"):
             loader.sampler.set_epoch(epoch)
         clip = _grad_clipper(self.model)
-        dev = next(self.model.parameters()).device
+        params = list(self.model.parameters())   # walked once per epoch, not per step
+        dev = params[0].device
         running = torch.zeros((), dtype=torch.float64, device=dev)
         n, start = 0, time.time()
         for i, batch in enumerate(loader):
@@ -218,7 +219,7 @@ class Solver(object):
                 loss.backward()
                 if getattr(self.model, "grad_sync", None) is not None:   # train.FlatDP
                     self.model.grad_sync.sync()
-                clip(self.model.parameters(), self.max_norm)
+                clip(params, self.max_norm)
                 self.optimizer.step()
             running += loss.detach().double()
             n = i + 1

@@ -88,8 +88,9 @@ def test_temporal_conv_net_vs_oracle(norm, causal, mask):
     import conv_tasnet as ct
     N, B, H, P, X, R, C, M, K = 32, 16, 32, 3, 3, 2, 2, 2, 250
     tcn = _randomize(ct.TemporalConvNet(N, B, H, P, X, R, C, norm, causal, mask), 9).to(DEV)
-    w = torch.rand(M, N, K) * 2
-    G = torch.randn(M, C, N, K)
+    gen = torch.Generator().manual_seed(17)   # fixed inputs (the global RNG depends on test order)
+    w = torch.rand(M, N, K, generator=gen) * 2
+    G = torch.randn(M, C, N, K, generator=gen)
     wg = w.to(DEV).requires_grad_(True)
     est = tcn(wg)
     assert est.shape == (M, C, N, K)
@@ -101,10 +102,9 @@ def test_temporal_conv_net_vs_oracle(norm, causal, mask):
     (er * G).sum().backward()
     assert rel(est.detach(), er.detach()) < 1e-4
     assert rel(wg.grad, wc.grad) < 2e-3
-    for n, p in tcn.named_parameters():
-        if p.numel() == 1:
-            continue
-        assert rel(p.grad, params["separator." + n].grad) < 2e-3, n
+    errs = {n: rel(p.grad, params["separator." + n].grad) for n, p in tcn.named_parameters() if p.numel() > 1}
+    bad = {n: e for n, e in errs.items() if e >= 2e-3}
+    assert not bad, (bad, max(errs.values()))
 
 
 def test_layers_bf16_close_to_fp32():

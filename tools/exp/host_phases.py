@@ -22,6 +22,7 @@ mix, src = synthetic.speech_like(M, C, T, 1234)
 mix, src = mix.to(dev), src.to(dev)
 lens = torch.full((M,), T, dtype=torch.int64, device=dev)
 ph = {}
+plist = list(model.parameters())   # as bench.py
 SYNC = "--sync" in sys.argv   # drain the GPU before each phase: host cost without queue back-pressure
 
 
@@ -40,7 +41,7 @@ def step(rec):
     loss = run("loss", lambda: pc.cal_loss(src, est, lens)[0])
     run("zero_grad", lambda: opt.zero_grad(set_to_none=True))
     run("backward", lambda: loss.backward())
-    run("clip", lambda: ctn_optim.clip_grad_norm_(model.parameters(), 5.0))
+    run("clip", lambda: ctn_optim.clip_grad_norm_(plist, 5.0))
     run("adam", lambda: opt.step())
     if rec:
         for n, v in times:
