@@ -99,6 +99,13 @@ build/dual_ws_nv_%: tools/microbench/dual_ws_bench.hip $(PKG)/csrc/ctn_dual_ws.h
 	  -DCTN_DV_EXP=$(word 4,$(subst _, ,$*)) -DCTN_DV_LA=$(word 5,$(subst _, ,$*)) $< -o $@
 
 .PHONY: dualwsnv
+
+# column waves' tiles per iteration: build/dual_ws_c2_<0|1>
+dualwsc2: build/dual_ws_c2_0 build/dual_ws_c2_1
+build/dual_ws_c2_%: tools/microbench/dual_ws_bench.hip $(PKG)/csrc/ctn_dual_ws.hip $(PKG)/csrc/ctn_gemm_dual.hip $(HDR)
+	@mkdir -p build
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -Iinclude $(DEVFLAGS) -DCTN_DV_C2=$* $< -o $@
+.PHONY: dualwsc2
 .PHONY: dualwsdbg
 
 # library variants for A/B runs (tools/gpu_variants.sh, loaded through CTN_HIP_LIB):

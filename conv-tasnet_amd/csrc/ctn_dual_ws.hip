@@ -124,6 +124,14 @@ static_assert(DV_CJC == 1 || DV_CJC == 2 || DV_CJC == 4, "column blocks per colu
 #define CTN_DV_CLNC 1
 #endif
 
+// Column waves: two tiles per loop iteration (experiment, off): measured slower, 106.5
+// against 81.3-82.8 us at the bench shape and 590 against 533-553 us at c4's
+// (microbenchmark, one box) — a wave holding two slots releases the older
+// one a tile later, which shortens the memory waves' look-ahead
+#ifndef CTN_DV_C2
+#define CTN_DV_C2 0
+#endif
+
 // Row waves: A fragments read LA k-steps ahead of their MFMAs
 #ifndef CTN_DV_LA
 #define CTN_DV_LA 1
@@ -536,62 +544,102 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
       cb[j] = COLS ? 0.f : sgb[1][16 * (CJ * wn + j) + lr];
     }
     const float bal = COLS ? 0.f : p.bop.alpha[0];
-    auto run = [&](auto le1) __attribute__((always_inline)) {
+    // one tile's B fragments (raw d -> op(d) for RAWB=1), read from the ring slot at `base`
+    auto load_b = [&](auto le1, int t, const char* base, bf16x8_t* bfr) __attribute__((always_inline)) {
       constexpr bool LE1 = decltype(le1)::value;
+      const char* bb = base + OFF_B;
+#pragma unroll
+      for (int j = 0; j < CJ; ++j) {
+        const s16x4_t lo = dv_tr(bb + (DV_RB ? bbase[0] ^ (j << 5) : bbase[0] + j * DV_BST));
+        const s16x4_t hi = dv_tr(bb + (DV_RB ? bbase[1] ^ (j << 5) : bbase[1] + j * DV_BST));
+        bfr[j] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+      if constexpr (DV_RB && !COLS && !DV_NI) {
+        float mu[8], rs[8];
+        if constexpr (NK == NORM_GLN) {
+          const float2 st = *reinterpret_cast<const float2*>(base + OFF_ST);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) mu[e] = st.x, rs[e] = st.y;
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float4 st = *reinterpret_cast<const float4*>(base + OFF_ST + 64 * lg + 16 * k);
+            mu[2 * k] = st.x, rs[2 * k] = st.y, mu[2 * k + 1] = st.z, rs[2 * k + 1] = st.w;
+          }
+        }
+        const int tk = (t * TM) % Kp;
+#pragma unroll
+        for (int j = 0; j < CJ; ++j) {
+          v4u v = __builtin_bit_cast(v4u, bfr[j]);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            float x0 = __uint_as_float(v[k] << 16), x1 = __uint_as_float(v[k] & 0xffff0000u);
+            x0 = dv_prelu<LE1>(x0, bal);
+            x1 = dv_prelu<LE1>(x1, bal);
+            x0 = fmaf(x0 - mu[2 * k], rs[2 * k] * cg[j], cb[j]);
+            x1 = fmaf(x1 - mu[2 * k + 1], rs[2 * k + 1] * cg[j], cb[j]);
+            if constexpr (NK == NORM_CLN) {   // padded frames: statistics not finite
+              if (tk + 8 * lg + 2 * k >= Kv) x0 = 0.f;
+              if (tk + 8 * lg + 2 * k + 1 >= Kv) x1 = 0.f;
+            }
+            v[k] = pk_bf16(x0, x1);
+          }
+          bfr[j] = __builtin_bit_cast(bf16x8_t, v);
+        }
+      }
+    };
+    auto a_frag = [&](const char* base, int i) __attribute__((always_inline)) {
+      const int o = (i >> 1) * 1024 + (i & 1) * 512;
+      const s16x4_t lo = dv_tr(base + OFF_A + abase[0] + o), hi = dv_tr(base + OFF_A + abase[1] + o);
+      return bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    };
+    // NIMG: the row waves' DONE of the tile (they waited for FULL and wrote op(d))
+    auto full_word = [&](int slot) __attribute__((always_inline)) {
+      return (DV_NI && !COLS) ? fl_done[slot] : fl_full[slot];
+    };
+    auto run = [&](auto le1) __attribute__((always_inline)) {
       int slot = 0;
       uint32_t gen = 1;
-      for (int t = t0; t < t1; ++t) {
-        // NIMG: the row waves' DONE of the tile (they waited for FULL and wrote op(d))
-        dv_wait<4>((DV_NI && !COLS) ? fl_done[slot] : fl_full[slot], gen, p.err);
-        const char* base = smem + slot * SLOT;
-        if constexpr (!(CTN_DV_EXP & 3)) {
-          const char* a = base + OFF_A;
-          const char* bb = base + OFF_B;
-          bf16x8_t bfr[CJ];
-#pragma unroll
-          for (int j = 0; j < CJ; ++j) {
-            const s16x4_t lo = dv_tr(bb + (DV_RB ? bbase[0] ^ (j << 5) : bbase[0] + j * DV_BST));
-            const s16x4_t hi = dv_tr(bb + (DV_RB ? bbase[1] ^ (j << 5) : bbase[1] + j * DV_BST));
-            bfr[j] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          }
-          if constexpr (DV_RB && !COLS && !DV_NI) {
-            float mu[8], rs[8];
-            if constexpr (NK == NORM_GLN) {
-              const float2 st = *reinterpret_cast<const float2*>(base + OFF_ST);
-#pragma unroll
-              for (int e = 0; e < 8; ++e) mu[e] = st.x, rs[e] = st.y;
-            } else {
-#pragma unroll
-              for (int k = 0; k < 4; ++k) {
-                const float4 st = *reinterpret_cast<const float4*>(base + OFF_ST + 64 * lg + 16 * k);
-                mu[2 * k] = st.x, rs[2 * k] = st.y, mu[2 * k + 1] = st.z, rs[2 * k + 1] = st.w;
-              }
-            }
-            const int tk = (t * TM) % Kp;
-#pragma unroll
-            for (int j = 0; j < CJ; ++j) {
-              v4u v = __builtin_bit_cast(v4u, bfr[j]);
-#pragma unroll
-              for (int k = 0; k < 4; ++k) {
-                float x0 = __uint_as_float(v[k] << 16), x1 = __uint_as_float(v[k] & 0xffff0000u);
-                x0 = dv_prelu<LE1>(x0, bal);
-                x1 = dv_prelu<LE1>(x1, bal);
-                x0 = fmaf(x0 - mu[2 * k], rs[2 * k] * cg[j], cb[j]);
-                x1 = fmaf(x1 - mu[2 * k + 1], rs[2 * k + 1] * cg[j], cb[j]);
-                if constexpr (NK == NORM_CLN) {   // padded frames: statistics not finite
-                  if (tk + 8 * lg + 2 * k >= Kv) x0 = 0.f;
-                  if (tk + 8 * lg + 2 * k + 1 >= Kv) x1 = 0.f;
-                }
-                v[k] = pk_bf16(x0, x1);
-              }
-              bfr[j] = __builtin_bit_cast(bf16x8_t, v);
-            }
-          }
+      int t = t0;
+      // CTN_DV_C2: two tiles per iteration (two independent wait / transform / read chains
+      // in flight per wave); each accumulator still takes tile t before tile t + 1, so the
+      // partial sums keep their order
+      if constexpr (CTN_DV_C2 && !(CTN_DV_EXP & 3)) {
+        for (; t + 1 < t1; t += 2) {
+          const int s0 = slot;
+          const uint32_t g0 = gen;
+          if (++slot == NSL) slot = 0, ++gen;
+          const int s1 = slot;
+          const uint32_t g1 = gen;
+          if (++slot == NSL) slot = 0, ++gen;
+          const char* b0 = smem + s0 * SLOT;
+          const char* b1 = smem + s1 * SLOT;
+          bf16x8_t bf0[CJ], bf1[CJ];
+          dv_wait<4>(full_word(s0), g0, p.err);
+          load_b(le1, t, b0, bf0);
+          dv_wait<4>(full_word(s1), g1, p.err);
+          load_b(le1, t + 1, b1, bf1);
 #pragma unroll
           for (int i = 0; i < CI; ++i) {
-            const int o = (i >> 1) * 1024 + (i & 1) * 512;
-            const s16x4_t lo = dv_tr(a + abase[0] + o), hi = dv_tr(a + abase[1] + o);
-            const bf16x8_t af = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            const bf16x8_t a0 = a_frag(b0, i), a1 = a_frag(b1, i);
+#pragma unroll
+            for (int j = 0; j < CJ; ++j) dacc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf0[j], dacc[i][j], 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < CJ; ++j) dacc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf1[j], dacc[i][j], 0, 0, 0);
+          }
+          dv_signal(&fl_done[s0][NR + c], g0);
+          dv_signal(&fl_done[s1][NR + c], g1);
+        }
+      }
+      for (; t < t1; ++t) {
+        dv_wait<4>(full_word(slot), gen, p.err);
+        const char* base = smem + slot * SLOT;
+        if constexpr (!(CTN_DV_EXP & 3)) {
+          bf16x8_t bfr[CJ];
+          load_b(le1, t, base, bfr);
+#pragma unroll
+          for (int i = 0; i < CI; ++i) {
+            const bf16x8_t af = a_frag(base, i);
 #pragma unroll
             for (int j = 0; j < CJ; ++j) dacc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], dacc[i][j], 0, 0, 0);
           }
