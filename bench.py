@@ -508,8 +508,8 @@ def main():
                                     f"{'causal' if cfg['causal'] else 'non-causal'} relu-mask, {C} spk, "
                                     f"{args.seconds:g} s @ {rate // 1000} kHz, fwd+PIT loss+bwd+clip+Adam"),
                        "per_gpu_batch": M, "global_batch": M * world, "samples": T, "frames": K,
-                       "parallelism": f"dp{world}" + ((" (DDP/RCCL)" if grad_sync is None else
-                                                                     " (flat all-reduce/RCCL)") if use_ddp else "")
+                       "parallelism": f"dp{world}" + ((" (DDP/" if grad_sync is None else " (flat all-reduce/")
+                                                      + ("gloo)" if _rehearsal() else "RCCL)") if use_ddp else "")
                                       + (" REHEARSAL: all ranks on one GPU over gloo" if _rehearsal() else ""),
                        "rccl_world_size": dist.get_world_size() if use_ddp and not _rehearsal() else None,
                        "rank_ms_per_step": rank_ms,
