@@ -596,6 +596,14 @@ __global__ __launch_bounds__(256) void dec_bwd_mfma_kernel(CodecArgs a) {
     const int er = lane >> 2, en = 8 * (lane & 3);   // element-wise row / first channel in the round
 #pragma unroll 1
     for (int nb = 0; nb < NBN; nb += 2) {
+      const long r = r0 + er;
+      const int n0 = nb * 16 + en;
+      // the round's mixture-weight and score rows are loaded before its MFMAs and tile
+      // stage (which end in a compiler barrier): their latency overlaps that work
+      const v4u wraw = ldg16(w + r * N + n0);
+      v4u sraw[CM];
+#pragma unroll
+      for (int c = 0; c < CM; ++c) sraw[c] = c < C ? ldg16(sc + r * (long)(C * N) + (long)c * N + n0) : v4u{0u, 0u, 0u, 0u};
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -607,14 +615,12 @@ __global__ __launch_bounds__(256) void dec_bwd_mfma_kernel(CodecArgs a) {
             *reinterpret_cast<float4*>(tile + (c * 16 + lr) * TS + h * 16 + 4 * lg) = float4{g[0], g[1], g[2], g[3]};
           }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the wave's own tile: no barrier needed
-      const long r = r0 + er;
-      const int n0 = nb * 16 + en;
       float wf[8], sv[CM][8], gs[CM][8];
-      unpack_bf16x8(ldg16(w + r * N + n0), wf);
+      unpack_bf16x8(wraw, wf);
 #pragma unroll
       for (int c = 0; c < CM; ++c)
         if (c < C) {
-          unpack_bf16x8(ldg16(sc + r * (long)(C * N) + (long)c * N + n0), sv[c]);
+          unpack_bf16x8(sraw[c], sv[c]);
           const float4 g0 = *reinterpret_cast<const float4*>(tile + (c * 16 + er) * TS + en);
           const float4 g1 = *reinterpret_cast<const float4*>(tile + (c * 16 + er) * TS + en + 4);
           gs[c][0] = g0.x; gs[c][1] = g0.y; gs[c][2] = g0.z; gs[c][3] = g0.w;
