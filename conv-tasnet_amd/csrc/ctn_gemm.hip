@@ -639,7 +639,10 @@ __global__ __launch_bounds__(256 * ColsCks<T>::v) void gemm_cols_kernel(GemmCols
   // previous barrier).  The loop is unrolled by NSET so every set index is static.
   // Rows of padded frames are zero in the plain operands of this path, so they add
   // nothing; transformed operands are zeroed there explicitly.
-  constexpr int NSET = 2;   // deeper rings measured slower (register pressure)
+#ifndef CTN_COLS_NSET
+#define CTN_COLS_NSET 2
+#endif
+  constexpr int NSET = CTN_COLS_NSET;   // register sets in flight (experiment switch)
   // Both groups run nks_all rounds in lock step (the barriers are workgroup-wide);
   // a group with fewer steps keeps staging its clamped last step but skips the
   // MFMAs of the surplus rounds (a wave-uniform branch after the barrier).
@@ -651,18 +654,20 @@ __global__ __launch_bounds__(256 * ColsCks<T>::v) void gemm_cols_kernel(GemmCols
     for (; ks + NSET - 1 < nks_all; ks += NSET) {   // full rounds: the same loads trail every wait
 #pragma unroll
       for (int u = 0; u < NSET; ++u) {
-        swrite(le1, R[u], ks + u, smem + (u & 1) * STAGE);
+        char* st = smem + ((ks + u) & 1) * STAGE;
+        swrite(le1, R[u], ks + u, st);
         gload(R[u], ks + u + NSET);
         lds_barrier();
-        if (ks + u < nks) compute(smem + (u & 1) * STAGE);
+        if (ks + u < nks) compute(st);
       }
     }
 #pragma unroll
-    for (int u = 0; u < NSET; ++u) {   // tail (ks is a multiple of NSET, so parity = u & 1)
+    for (int u = 0; u < NSET; ++u) {   // tail
       if (ks + u < nks_all) {
-        swrite(le1, R[u], ks + u, smem + (u & 1) * STAGE);
+        char* st = smem + ((ks + u) & 1) * STAGE;
+        swrite(le1, R[u], ks + u, st);
         lds_barrier();
-        if (ks + u < nks) compute(smem + (u & 1) * STAGE);
+        if (ks + u < nks) compute(st);
       }
     }
   };
