@@ -443,11 +443,17 @@ template <> CTN_DEV int cswz<float>(int row, int col) { return row * ColsPitch<f
 #define CTN_COLS_CKS 2   // bf16 k-split groups per workgroup (experiment switch)
 #endif
 template <typename T> struct ColsCks { static constexpr int v = sizeof(T) == 2 ? CTN_COLS_CKS : 2; };
+#ifndef CTN_COLS_CKR
+#define CTN_COLS_CKR 32  // bf16 frame rows per k-step (experiment switch: 32 or 64)
+#endif
+template <typename T> struct ColsCkr { static constexpr int v = sizeof(T) == 2 ? CTN_COLS_CKR : CKR; };
 constexpr int CKS = 2;                           // k-split groups per workgroup (host-side sizing)
 
 template <typename T, int OPA, int OPB, int NK>
 __global__ __launch_bounds__(256 * ColsCks<T>::v) void gemm_cols_kernel(GemmCols p) {
   constexpr int CKS = ColsCks<T>::v;
+  constexpr int CKR = ColsCkr<T>::v;
+  static_assert(CKR % 32 == 0, "k-steps are whole 32-row MFMA steps");
   constexpr int PITCH = ColsPitch<T>::v;
   constexpr int STAGE = 2 * CKR * PITCH;         // one k-step: A tile then B tile
   static_assert(CKS * 2 * STAGE >= CBP * CBQ * 4, "accumulator exchange (one group at a time) fits the stages");
@@ -590,30 +596,33 @@ __global__ __launch_bounds__(256 * ColsCks<T>::v) void gemm_cols_kernel(GemmCols
     if constexpr (sizeof(T) == 2) {
       // transposed LDS reads: lane (g, 4q+pp) addresses row 8g+4h+q, columns 4pp..4pp+3
       const int q = lr >> 2, pp = lr & 3;
-      bf16x8_t af[4], bfr[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int col = wp * 64 + i * 16 + 4 * pp;
-        s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) s16x4_t*)(sA + cswz<T>(8 * lg + q, col)));
-        s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) s16x4_t*)(sA + cswz<T>(8 * lg + 4 + q, col)));
-        af[i] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      for (int k32 = 0; k32 < CKR; k32 += 32) {
+        bf16x8_t af[4], bfr[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int col = wp * 64 + i * 16 + 4 * pp;
+          s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4_t*)(sA + cswz<T>(k32 + 8 * lg + q, col)));
+          s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4_t*)(sA + cswz<T>(k32 + 8 * lg + 4 + q, col)));
+          af[i] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int col = wq * 64 + j * 16 + 4 * pp;
+          s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4_t*)(sB + cswz<T>(k32 + 8 * lg + q, col)));
+          s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4_t*)(sB + cswz<T>(k32 + 8 * lg + 4 + q, col)));
+          bfr[j] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int col = wq * 64 + j * 16 + 4 * pp;
-        s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) s16x4_t*)(sB + cswz<T>(8 * lg + q, col)));
-        s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) s16x4_t*)(sB + cswz<T>(8 * lg + 4 + q, col)));
-        bfr[j] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     } else {
 #pragma unroll
       for (int k4 = 0; k4 < CKR; k4 += 4) {
@@ -759,7 +768,7 @@ int gemm_cols_chunks(DType dt, const GemmCols& p) {
 
 hipError_t launch_gemm_cols(DType dt, const GemmCols& p, hipStream_t s) {
   if (gemm_cols_ws_eligible(dt, p) && p.nchunks == gemm_cols_ws_ranges(p)) return launch_gemm_cols_ws(p, s);
-  if (p.g.Kp % CKR != 0 || p.P % 8 != 0 || p.Q % 8 != 0 || p.nchunks < 1 || p.g.rows() >= (1L << 31))
+  if (p.g.Kp % (dt == BF16 ? ColsCkr<bf16raw>::v : CKR) != 0 || p.P % 8 != 0 || p.Q % 8 != 0 || p.nchunks < 1 || p.g.rows() >= (1L << 31))
     return hipErrorInvalidValue;
   const int nk = p.bop.kind != OP_PLAIN ? p.bop.norm : 0;
   if (dt == BF16)
