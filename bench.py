@@ -292,6 +292,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--timer-kind", type=int, default=0,
                     help="kernel timed in the timed region (default: the dominant one of the profile pass)")
+    ap.add_argument("--timer-stride", type=int, default=9,
+                    help="in the timed region, bracket every n-th launch of the timed kernel with "
+                         "hipEvents (each bracket idles the GPU a few us around the launch); 9 is "
+                         "coprime with the 32 launches per step, so the samples visit every block")
     ap.add_argument("--profile-steps", type=int, default=5,
                     help="untimed steps with every kernel family timed (the per-kernel table)")
     ap.add_argument("--ddp", action="store_true",
@@ -433,6 +437,7 @@ def main():
         graph = ctn_graph.StepGraph(step, warmup=1)   # one more eager step on a side stream, then capture
     torch.cuda.synchronize(dev)
     if graph is None:   # (a replay re-runs the captured launches: the live timer sees none of them)
+        L.check(lib.ctn_timer_set_stride(args.timer_stride), "ctn_timer_set_stride")
         L.check(lib.ctn_timer_enable(args.timer_kind, args.steps * 64), "ctn_timer_enable")
     if use_ddp:
         dist.barrier()
@@ -448,6 +453,7 @@ def main():
     nl = ctypes.c_int(0)
     L.check(lib.ctn_timer_read(ctypes.byref(tot), ctypes.byref(nl)), "ctn_timer_read")
     lib.ctn_timer_enable(0, 0)
+    lib.ctn_timer_set_stride(1)
     # a generation-word timeout anywhere in the run fails the bench (ctn_device_status)
     L.check(lib.ctn_device_status(ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream), None, 0),
             "ctn_device_status")
@@ -525,7 +531,7 @@ def main():
                          "gemm_ws bwd g_n2 = gy.W2 (norm-backward epilogue)",
                          # measured streaming ceiling on this GPU (device copy, read + write)
                          "copy_peak": round(copy_gbs, 1), "frac_of_copy_peak": round(achieved / copy_gbs, 4),
-                         "launches": nl.value, "mean_ms": round(mean_ms, 4), "bytes_per_launch": kb,
+                         "launches": nl.value, "timer_stride": args.timer_stride, "mean_ms": round(mean_ms, 4), "bytes_per_launch": kb,
                          # rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * 1024 SIMDs) of
                          # this kernel, from the committed PMC pass (profiles/pmc_mfma.json)
                          "mfma_util": mfma.get("mfma_util") if mfma else None,

@@ -45,7 +45,9 @@ struct Timer {
   std::mutex mu;
   uint32_t mask = 0;
   int cap = 0;                              // launches per kind
+  int stride = 1;                           // bracket every stride-th launch of a kind
   int used[32] = {};
+  long seen[32] = {};                       // launches of a kind since enable
   std::vector<hipEvent_t> ev[32];           // pairs
 };
 Timer g_timer;
@@ -56,7 +58,7 @@ struct TimedScope {
   TimedScope(int k, hipStream_t st) : s(st), kind(k) {
     if (k <= 0 || k >= 32 || !((g_timer.mask >> k) & 1u)) return;
     std::lock_guard<std::mutex> lk(g_timer.mu);
-    if (g_timer.used[k] >= g_timer.cap) return;
+    if (g_timer.seen[k]++ % g_timer.stride != 0 || g_timer.used[k] >= g_timer.cap) return;
     idx = g_timer.used[k]++;
     (void)hipEventRecord(g_timer.ev[k][2 * idx], s);
   }
@@ -73,6 +75,7 @@ extern "C" int ctn_timer_enable_mask(uint32_t mask, int max_launches) {
     for (auto e : g_timer.ev[k]) (void)hipEventDestroy(e);
     g_timer.ev[k].clear();
     g_timer.used[k] = 0;
+    g_timer.seen[k] = 0;
   }
   g_timer.mask = max_launches ? mask : 0u;
   g_timer.cap = max_launches;
@@ -81,6 +84,13 @@ extern "C" int ctn_timer_enable_mask(uint32_t mask, int max_launches) {
     g_timer.ev[k].resize(2 * (size_t)g_timer.cap);
     for (auto& e : g_timer.ev[k]) CTN_HIP(hipEventCreate(&e));
   }
+  return CTN_OK;
+}
+
+extern "C" int ctn_timer_set_stride(int stride) {
+  if (stride < 1) return fail(CTN_ERR_ARG, "timer stride %d", stride);
+  std::lock_guard<std::mutex> lk(g_timer.mu);
+  g_timer.stride = stride;
   return CTN_OK;
 }
 

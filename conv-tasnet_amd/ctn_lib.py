@@ -14,7 +14,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CTN_HIP_LIB", os.path.join(_HERE, "libctn_hip.so"))
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 DTYPE_F32, DTYPE_BF16 = 0, 1
 NORM_GLN, NORM_CLN, NORM_BN = 0, 1, 2
@@ -173,6 +173,7 @@ _SIGS = {
     "ctn_stream_call": (ctypes.c_int, [c_void_p, c_void_p, ctypes.c_int64, c_void_p, ctypes.c_int64] + [c_void_p] * 4 +
                         [c_size_t, c_void_p]),
     "ctn_timer_enable": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    "ctn_timer_set_stride": (ctypes.c_int, [ctypes.c_int]),
     "ctn_timer_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
     "ctn_timer_enable_mask": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_int]),
     "ctn_timer_read_kind": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_double),

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define CTN_ABI_VERSION 10
+#define CTN_ABI_VERSION 11
 
 typedef enum { CTN_DTYPE_F32 = 0, CTN_DTYPE_BF16 = 1 } ctn_dtype;
 /* CTN_NORM_BN: torch.nn.BatchNorm1d, chose_norm's fallback branch (conv_tasnet.py:302-303) */
@@ -427,6 +427,11 @@ int ctn_timer_enable(int kind, int max_launches);
 int ctn_timer_enable_mask(uint32_t mask, int max_launches);
 int ctn_timer_read(double* total_ms, int* launches);              /* all kinds */
 int ctn_timer_read_kind(int kind, double* total_ms, int* launches);
+/* ABI v11: bracket only every stride-th launch of each enabled kind (stride >= 1,
+ * default 1; counted from the last enable).  Each bracketing event pair leaves the GPU
+ * idle for a few microseconds around the launch, so a sampled timer perturbs the
+ * measured run less; read_kind then reports the sampled launches. */
+int ctn_timer_set_stride(int stride);
 
 /* -------------------------------------------------------------------------
  * Device error word (ABI v9).  Kernels whose waves hand tiles to each other through

@@ -106,6 +106,13 @@ def test_timer_off_by_default(lib):
     assert n.value == 0 and tot.value == 0.0
 
 
+def test_timer_stride_validation(lib):
+    assert lib.ctn_timer_set_stride(0) != 0
+    assert "stride" in lib.ctn_last_error().decode()
+    assert lib.ctn_timer_set_stride(8) == 0
+    assert lib.ctn_timer_set_stride(1) == 0
+
+
 def test_pack_weights_validation(lib):
     """ctn_pack_weights checks its table before launching anything: an entry needs a
     destination, and the fragment-order copies need rows and cols in multiples of 32."""
