@@ -86,23 +86,43 @@ def kernel_bytes(kind, M, K, cfg, s=2):
     raise ValueError(kind)
 
 
-def copy_peak_gbs(dev, mib=1024, reps=10):
-    """Measured streaming ceiling of this GPU: a device-to-device copy of `mib` MiB
-    (read + write bytes / time, best of `reps`), SURVEY.md §8(d)'s measured peak beside
-    the 8 TB/s datasheet value."""
-    n = mib * (1 << 20) // 4
-    a = torch.empty(n, dtype=torch.float32, device=dev).uniform_()
-    b = torch.empty_like(a)
-    best = float("inf")
-    for _ in range(reps + 2):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        b.copy_(a)
-        e1.record()
-        e1.synchronize()
-        best = min(best, e0.elapsed_time(e1))
-    del a, b
-    return 2 * n * 4 / (best * 1e-3) / 1e9
+def copy_peak_gbs(dev, lib, sizes_mib=(256, 512, 1024), reps=10):
+    """Measured streaming ceiling of this GPU: device-to-device copies (read + write bytes
+    / time, best of `reps`) by torch's copy_ and by the library's 16-B-per-lane copy kernel
+    (ctn_copy_bytes: grid-stride or one chunk per lane, with and without the nontemporal
+    hint, 4 or 8 loads in flight) over buffers of 256 MiB to 1 GiB — the block kernels move
+    157-420 MB per launch — SURVEY.md §8(d)'s measured peak beside the 8 TB/s datasheet
+    value.  The best rate over all of them is the ceiling.  Returns (GB/s, which copy)."""
+    import ctn_lib as L
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    res = {}
+    for mib in sizes_mib:
+        n = mib * (1 << 20) // 4
+        a = torch.empty(n, dtype=torch.float32, device=dev).uniform_()
+        b = torch.empty_like(a)
+        ways = {"torch copy_": lambda: b.copy_(a)}
+        for fl in range(4):   # flags: nontemporal, 8 loads in flight
+            per_wg = 256 * (8 if fl & 2 else 4) * 4          # floats one workgroup moves per round
+            for wgs in (2048, 4096, min(65536, (n + per_wg - 1) // per_wg)):
+                ways[f"ctn_copy_bytes wg={wgs} flags={fl}"] = (lambda w, f: lambda: L.check(
+                    lib.ctn_copy_bytes(b.data_ptr(), a.data_ptr(), n * 4, w, f, stream), "ctn_copy_bytes"))(wgs, fl)
+        for name, fn in ways.items():
+            best = float("inf")
+            for _ in range(reps + 2):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                fn()
+                e1.record()
+                e1.synchronize()
+                best = min(best, e0.elapsed_time(e1))
+            res[f"{name} {mib} MiB"] = 2 * n * 4 / (best * 1e-3) / 1e9
+        if not torch.equal(a, b):
+            raise RuntimeError("bench.py: the calibration copy is wrong")
+        del a, b
+    name = max(res, key=res.get)
+    if os.environ.get("CTN_COPY_VERBOSE"):
+        print(json.dumps({k: round(v, 1) for k, v in res.items()}), file=sys.stderr)
+    return res[name], name
 
 
 def dual_pair_a():
@@ -467,7 +487,7 @@ def main():
         elapsed = max(float(x) for x in ts)
     final_loss = float(loss.detach())
     deferred = (ctn_ops.DEFERRED_BLOCKS - n_def0) / args.steps
-    copy_gbs = copy_peak_gbs(dev) if rank == 0 else None
+    copy_gbs, copy_how = copy_peak_gbs(dev, lib) if rank == 0 else (None, None)
 
     if rank == 0:
         s = s_el
@@ -530,7 +550,7 @@ def main():
                                                                         not dual_pair_a()) else
                          "gemm_ws bwd g_n2 = gy.W2 (norm-backward epilogue)",
                          # measured streaming ceiling on this GPU (device copy, read + write)
-                         "copy_peak": round(copy_gbs, 1), "frac_of_copy_peak": round(achieved / copy_gbs, 4),
+                         "copy_peak": round(copy_gbs, 1), "copy_peak_by": copy_how, "frac_of_copy_peak": round(achieved / copy_gbs, 4),
                          "launches": nl.value, "timer_stride": args.timer_stride, "mean_ms": round(mean_ms, 4), "bytes_per_launch": kb,
                          # rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * 1024 SIMDs) of
                          # this kernel, from the committed PMC pass (profiles/pmc_mfma.json)

@@ -94,6 +94,15 @@ extern "C" int ctn_timer_set_stride(int stride) {
   return CTN_OK;
 }
 
+extern "C" int ctn_copy_bytes(void* dst, const void* src, size_t bytes, int workgroups, int flags, void* stream) {
+  if (!dst || !src || bytes % 16 || ((uintptr_t)dst | (uintptr_t)src) % 16 || workgroups < 1 ||
+      workgroups > 65536 || (flags & ~3))
+    return fail(CTN_ERR_ARG, "copy: %zu bytes, %d workgroups, flags %d (16-byte multiples and alignment, 1..65536, "
+                "flags 0..3)", bytes, workgroups, flags);
+  CTN_HIP(ctn::launch_copy_stream(dst, src, bytes, workgroups, flags, (hipStream_t)stream));
+  return CTN_OK;
+}
+
 extern "C" int ctn_timer_enable(int kind, int max_launches) {
   if (kind < 0 || kind >= 32) return fail(CTN_ERR_ARG, "timer kind %d", kind);
   return ctn_timer_enable_mask(kind ? 1u << kind : 0u, kind ? max_launches : 0);

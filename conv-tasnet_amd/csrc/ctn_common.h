@@ -58,8 +58,28 @@ template <> struct Vec8<bf16raw> {
 // memcpy's, so arrays of them stay in registers (a struct copy can keep an
 // alloca alive in scratch or LDS).
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-CTN_DEV v4u ldg16(const void* p) { return *reinterpret_cast<const v4u*>(p); }
-CTN_DEV void stg16(void* p, v4u v) { *reinterpret_cast<v4u*>(p) = v; }
+// CTN_NT bits (experiment switch): 1 = 16-byte loads, 2 = 16-byte stores carry the
+// nontemporal hint
+#ifndef CTN_NT
+#define CTN_NT 0
+#endif
+CTN_DEV v4u ldg16(const void* p) {
+  if constexpr (CTN_NT & 1) return __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+  else return *reinterpret_cast<const v4u*>(p);
+}
+CTN_DEV void stg16(void* p, v4u v) {
+  if constexpr (CTN_NT & 2) __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(p));
+  else *reinterpret_cast<v4u*>(p) = v;
+}
+// the same with the nontemporal hint when NT (per-kernel choice)
+template <bool NT> CTN_DEV v4u ldg16h(const void* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+  else return ldg16(p);
+}
+template <bool NT> CTN_DEV void stg16h(void* p, v4u v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(p));
+  else stg16(p, v);
+}
 CTN_DEV void unpack_bf16x8(const v4u& v, float f[8]) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {

@@ -91,6 +91,12 @@ constexpr int WS_FOLD_MAX = 512;   // utterances whose gLN operand stats a workg
 #define CTN_WS_LA8 3
 #endif
 // experiment: 1 raises the wave priority (s_setprio 1) while it issues a tile's MFMAs
+// Nontemporal hints per configuration (bits): 1 = the resident-weight loads of the
+// forward B -> H GEMM (plain operand, PReLU-statistics epilogue), 2 = the output stores
+// of the forward H -> B GEMM (norm-2 operand, residual epilogue)
+#ifndef CTN_WS_NT
+#define CTN_WS_NT 0
+#endif
 #ifndef CTN_WS_PRIO
 #define CTN_WS_PRIO 0
 #endif
@@ -190,13 +196,15 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
   // fragment: half the L2 lines of the row-major reads, whose 64-byte row pieces fill
   // only half of each line; every CU reads the whole weight, so this read is a fixed
   // cost of the launch, 12.9 -> 7.8 us at one tile per workgroup)
+  constexpr bool NTW = (CTN_WS_NT & 1) && OPK == OP_PLAIN && EPI == EPI_PRELU_STATS;
+  constexpr bool NTO = (CTN_WS_NT & 2) && OPK == OP_PRELU_NORM;
   v4u wf[NB][KB];
   const bf16raw* WF = NB == 2 ? reinterpret_cast<const bf16raw*>(p.Wf) : nullptr;
   if (WF) {
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
-      for (int kb = 0; kb < KB; ++kb) wf[nb][kb] = ldg16(WF + frag_offset(sl * WV + wid, nb, kb, lane, KR));
+      for (int kb = 0; kb < KB; ++kb) wf[nb][kb] = ldg16h<NTW>(WF + frag_offset(sl * WV + wid, nb, kb, lane, KR));
   } else {
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
@@ -208,7 +216,7 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
         const int kr = (CTN_WS_EXP & 512) ? (kb + (int)blockIdx.x) % KB : kb;
         if constexpr (CTN_WS_EXP & 256) wf[nb][kb] = ldg16(W + ((size_t)((wid * NB + nb) * KB + kr) * 64 + lane) * 8);
         else wf[nb][kb] = ldg16(W + (size_t)n * p.ldw + kr * 32 + lg * 8);
-      } else wf[nb][kb] = ldg16(W + (size_t)n * p.ldw + kb * 32 + lg * 8);
+      } else wf[nb][kb] = ldg16h<NTW>(W + (size_t)n * p.ldw + kb * 32 + lg * 8);
   }
   }
 
@@ -475,7 +483,7 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
       bf16raw* dst = Cp + (size_t)(t * TM + mb * 16 + lr) * p.ldc + colbase;
 #pragma unroll
       for (int q = 0; q < Q; ++q)
-        if constexpr (!(CTN_WS_EXP & 1)) stg16(dst + q * 8, ov[mb][q]);
+        if constexpr (!(CTN_WS_EXP & 1)) stg16h<NTO>(dst + q * 8, ov[mb][q]);
     }
   };
   auto epilogue_math = [&](auto le1, int t, const f32x4_t (&acc)[MB][NB]) __attribute__((always_inline)) {

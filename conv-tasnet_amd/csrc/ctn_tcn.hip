@@ -806,6 +806,44 @@ struct SrBatch {
   int nj;
 };
 
+// Streaming copy (bench.py's measured bandwidth ceiling, ctn_copy_bytes): 16 B per lane,
+// U independent loads in flight per lane before their stores, grid-stride; NT: the loads
+// and stores carry the nontemporal hint.
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void copy_stream_kernel(const v4u* __restrict__ src, v4u* __restrict__ dst,
+                                                          long n16) {
+  const long stride = (long)gridDim.x * 256;
+  long i = (long)blockIdx.x * 256 + threadIdx.x;
+  for (; i + (U - 1) * stride < n16; i += U * stride) {
+    v4u v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = NT ? __builtin_nontemporal_load(src + i + u * stride) : src[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if constexpr (NT) __builtin_nontemporal_store(v[u], dst + i + u * stride);
+      else dst[i + u * stride] = v[u];
+    }
+  }
+  for (; i < n16; i += stride) dst[i] = src[i];
+}
+
+hipError_t launch_copy_stream(void* dst, const void* src, size_t bytes, int wgs, int flags, hipStream_t s) {
+  if (!dst || !src || bytes % 16 || ((uintptr_t)dst | (uintptr_t)src) % 16 || wgs < 1 || wgs > 65536 ||
+      (flags & ~3))
+    return hipErrorInvalidValue;
+  if (!bytes) return hipSuccess;
+  const v4u* a = (const v4u*)src;
+  v4u* b = (v4u*)dst;
+  const long n = (long)(bytes / 16);
+  switch (flags) {
+    case 0: hipLaunchKernelGGL((copy_stream_kernel<4, false>), dim3(wgs), dim3(256), 0, s, a, b, n); break;
+    case 1: hipLaunchKernelGGL((copy_stream_kernel<4, true>), dim3(wgs), dim3(256), 0, s, a, b, n); break;
+    case 2: hipLaunchKernelGGL((copy_stream_kernel<8, false>), dim3(wgs), dim3(256), 0, s, a, b, n); break;
+    default: hipLaunchKernelGGL((copy_stream_kernel<8, true>), dim3(wgs), dim3(256), 0, s, a, b, n); break;
+  }
+  return hipGetLastError();
+}
+
 __global__ __launch_bounds__(256) void slab_reduce_kernel(SrBatch b) {
   __shared__ double part[4][64];
   __shared__ double part4[4][4][64];

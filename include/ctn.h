@@ -432,6 +432,13 @@ int ctn_timer_read_kind(int kind, double* total_ms, int* launches);
  * idle for a few microseconds around the launch, so a sampled timer perturbs the
  * measured run less; read_kind then reports the sampled launches. */
 int ctn_timer_set_stride(int stride);
+/* ABI v11: a streaming device-to-device copy (16 B per lane, `workgroups` x 256 threads,
+ * grid-stride), bench.py's measured bandwidth ceiling beside the datasheet peak.  bytes,
+ * dst and src must be multiples of 16.  flags: bit 0 nontemporal loads and stores, bit 1
+ * eight loads in flight per lane instead of four. */
+#define CTN_COPY_NT 1
+#define CTN_COPY_DEEP 2
+int ctn_copy_bytes(void* dst, const void* src, size_t bytes, int workgroups, int flags, void* stream);
 
 /* -------------------------------------------------------------------------
  * Device error word (ABI v9).  Kernels whose waves hand tiles to each other through

@@ -113,6 +113,17 @@ def test_timer_stride_validation(lib):
     assert lib.ctn_timer_set_stride(1) == 0
 
 
+def test_copy_validation(lib):
+    """ctn_copy_bytes (bench calibration copy) checks sizes and alignment before launching."""
+    buf = ctypes.create_string_buffer(64)
+    p = ctypes.addressof(buf)
+    assert lib.ctn_copy_bytes(None, None, 16, 1, 0, None) == 1
+    assert lib.ctn_copy_bytes(p, p, 20, 1, 0, None) == 1       # not a multiple of 16
+    assert "16-byte" in lib.ctn_last_error().decode()
+    assert lib.ctn_copy_bytes(p, p, 16, 0, 0, None) == 1       # no workgroups
+    assert lib.ctn_copy_bytes(p, p, 16, 1, 4, None) == 1       # unknown flag
+
+
 def test_pack_weights_validation(lib):
     """ctn_pack_weights checks its table before launching anything: an entry needs a
     destination, and the fragment-order copies need rows and cols in multiples of 32."""
