@@ -143,6 +143,10 @@ constexpr int DV_LA = CTN_DV_LA;
 // bit 2 no epilogue math, bit 3 no C stores, bit 4 row waves store zeros and nothing else,
 // bit 5 the memory waves issue no DMA (consumers read whatever the ring holds), bit 6 the
 // row waves skip all arithmetic.
+// 1: the row waves' output (dL/dn2) stores carry the nontemporal hint
+#ifndef CTN_DV_NT
+#define CTN_DV_NT 0
+#endif
 #ifndef CTN_DV_EXP
 #define CTN_DV_EXP 0
 #endif
@@ -448,7 +452,8 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
             // whole 16-byte lanes straight to memory (a wave covers 16 rows x 64 B)
             if constexpr (!(CTN_DV_EXP & 8))
               // wave-uniform 64-bit tile base + 32-bit lane offset (SGPR base, one VGPR)
-              stg16(Cg + (size_t)t * TM * p.ldc + n0 + (uint32_t)((16 * rb + lr) * p.ldc + cl), (CTN_DV_DBG & 16) ? rw : cv);
+              stg16h<CTN_DV_NT != 0>(Cg + (size_t)t * TM * p.ldc + n0 + (uint32_t)((16 * rb + lr) * p.ldc + cl),
+                                     (CTN_DV_DBG & 16) ? rw : cv);
           }
           if constexpr (NK == NORM_GLN) {
             const int m = t / tpu;

@@ -58,8 +58,17 @@ CTN_DEV void unpack8(const v4u& v, float f[8]) { unpack_bf16x8(v, f); }
 // with 16 wait states after the store, or with a global store: tools/exp/dw_debug.py,
 // DESIGN.md §15).  The compiler inserts no wait state for it: its hazard model treats a
 // >64-bit MUBUF store with a register soffset as safe.
+// CTN_DW_NT bits: the nontemporal hint on the forward's d rows (1) and on the backward's
+// dL/da1 rows (2).  Both on: the rows stream past the Infinity Cache instead of evicting
+// what the next kernels read from it (dw_fwd 44.6 -> 38.4 us, the H -> B GEMM after it
+// 47.5 -> 42.5, dw_bwd 82.5 -> 80); the hint on the producers of h1, dL/dn2
+// or dL/dh1 slows their consumers instead.
+#ifndef CTN_DW_NT
+#define CTN_DW_NT 3
+#endif
+template <bool NT = false>
 CTN_DEV void row_store(void* base, v4u v, int row) {
-  stg16(reinterpret_cast<char*>(base) + (size_t)row * 1024 + (threadIdx.x & 63) * 16u, v);
+  stg16h<NT>(reinterpret_cast<char*>(base) + (size_t)row * 1024 + (threadIdx.x & 63) * 16u, v);
 }
 // a wave-uniform pair into scalar registers (readfirstlane works on 32-bit integers)
 CTN_DEV float2 uniform2(float2 v) {
@@ -188,7 +197,7 @@ __global__ __launch_bounds__(256, 4) void dw_fwd_wave_kernel(DwArgs a) {
       for (int e = 0; e < 8; ++e) o[e] = 0.f;
     }
     if (!EDGE || k < Kp)
-      row_store(a.d_out, pack_bf16x8v(o), it.base + k);
+      row_store<(CTN_DW_NT & 1) != 0>(a.d_out, pack_bf16x8v(o), it.base + k);
     if constexpr (NK == NORM_GLN) {
       ts += s;
       tss += ss;
@@ -529,7 +538,7 @@ __global__ __launch_bounds__(256, 2) void dw_bwd_wave_kernel(DwArgs a) {
       for (int e = 0; e < 8; ++e) ga1[e] = 0.f;
     }
     if (!EDGE || k < Kp)
-      row_store(a.ga1_out, pack_bf16x8v(ga1), it.base + k);
+      row_store<(CTN_DW_NT & 2) != 0>(a.ga1_out, pack_bf16x8v(ga1), it.base + k);
     (void)rh;
     if constexpr (NK == NORM_GLN) {
       ts += s;

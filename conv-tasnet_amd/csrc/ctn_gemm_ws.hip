@@ -93,7 +93,9 @@ constexpr int WS_FOLD_MAX = 512;   // utterances whose gLN operand stats a workg
 // experiment: 1 raises the wave priority (s_setprio 1) while it issues a tile's MFMAs
 // Nontemporal hints per configuration (bits): 1 = the resident-weight loads of the
 // forward B -> H GEMM (plain operand, PReLU-statistics epilogue), 2 = the output stores
-// of the forward H -> B GEMM (norm-2 operand, residual epilogue)
+// of the forward H -> B GEMM (norm-2 operand, residual epilogue), 4 = the output (h1)
+// stores of the forward B -> H GEMM, 8 = the dL/dh1 stores of the data-gradient GEMM
+// (norm-1-backward operand), 16 = that GEMM's output (gx) stores
 #ifndef CTN_WS_NT
 #define CTN_WS_NT 0
 #endif
@@ -197,7 +199,10 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
   // only half of each line; every CU reads the whole weight, so this read is a fixed
   // cost of the launch, 12.9 -> 7.8 us at one tile per workgroup)
   constexpr bool NTW = (CTN_WS_NT & 1) && OPK == OP_PLAIN && EPI == EPI_PRELU_STATS;
-  constexpr bool NTO = (CTN_WS_NT & 2) && OPK == OP_PRELU_NORM;
+  constexpr bool NTO = ((CTN_WS_NT & 2) && OPK == OP_PRELU_NORM) ||
+                      ((CTN_WS_NT & 4) && OPK == OP_PLAIN && EPI == EPI_PRELU_STATS) ||
+                      ((CTN_WS_NT & 16) && OPK == OP_NORM1_BWD);
+  constexpr bool NTG = (CTN_WS_NT & 8) != 0;
   v4u wf[NB][KB];
   const bf16raw* WF = NB == 2 ? reinterpret_cast<const bf16raw*>(p.Wf) : nullptr;
   if (WF) {
@@ -387,7 +392,7 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
     if constexpr (N1B && !(CTN_WS_EXP & 1024)) {   // bit 10 (timing only): no dL/dh1 stores
       if (tu < t1) {
 #pragma unroll
-        for (int j = 0; j < NA; ++j) stg16(GH + (size_t)(tu * TM + rl0 + j * RSTEP) * p.lda + kc * 8, ghv[j]);
+        for (int j = 0; j < NA; ++j) stg16h<NTG>(GH + (size_t)(tu * TM + rl0 + j * RSTEP) * p.lda + kc * 8, ghv[j]);
       }
     }
   };
