@@ -71,6 +71,18 @@ CTN_DEV void stg16(void* p, v4u v) {
   if constexpr (CTN_NT & 2) __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(p));
   else *reinterpret_cast<v4u*>(p) = v;
 }
+// CTN_PART_NT: fp32 split-K partial sums of the dual and column GEMMs (read back only by
+// the reductions at the end of the backward pass) stored with the nontemporal hint, so
+// they do not evict the activations the next kernels read from the Infinity Cache
+// (dw_bwd after the dual 85 -> 77 us, the dual itself +2.4, the column GEMM -1.5;
+// DESIGN.md §15)
+#ifndef CTN_PART_NT
+#define CTN_PART_NT 1
+#endif
+CTN_DEV void st_part(float* p, float v) {
+  if constexpr (CTN_PART_NT != 0) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
 // the same with the nontemporal hint when NT (per-kernel choice)
 template <bool NT> CTN_DEV v4u ldg16h(const void* p) {
   if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));

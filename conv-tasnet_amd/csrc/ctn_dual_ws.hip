@@ -683,7 +683,7 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
       for (int j = 0; j < CJ; ++j) {
         const int n = n0 + (wn * CJ + j) * 16 + lr;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) Dp[(size_t)((wp * CI + i) * 16 + 4 * lg + e) * p.Nout + n] = dacc[i][j][e];
+        for (int e = 0; e < 4; ++e) st_part(&Dp[(size_t)((wp * CI + i) * 16 + 4 * lg + e) * p.Nout + n], dacc[i][j][e]);
       }
     return;
   }

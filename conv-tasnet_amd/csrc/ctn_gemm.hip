@@ -719,7 +719,7 @@ __global__ __launch_bounds__(256 * ColsCks<T>::v) void gemm_cols_kernel(GemmCols
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int pr = p0 + wp * 64 + i * 16 + lg * 4 + e;
-        if (pr < p.P) Cp[(size_t)pr * p.Q + qq] = acc[i][j][e];
+        if (pr < p.P) st_part(&Cp[(size_t)pr * p.Q + qq], acc[i][j][e]);
       }
     }
 }
