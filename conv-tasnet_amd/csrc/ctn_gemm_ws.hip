@@ -95,9 +95,11 @@ constexpr int WS_FOLD_MAX = 512;   // utterances whose gLN operand stats a workg
 // forward B -> H GEMM (plain operand, PReLU-statistics epilogue), 2 = the output stores
 // of the forward H -> B GEMM (norm-2 operand, residual epilogue), 4 = the output (h1)
 // stores of the forward B -> H GEMM, 8 = the dL/dh1 stores of the data-gradient GEMM
-// (norm-1-backward operand), 16 = that GEMM's output (gx) stores
+// (norm-1-backward operand), 16 = that GEMM's output (gx) stores, 32 = that GEMM's
+// dL/da1 operand loads (its last use; measured -1.7 us, the others slower or flat:
+// profiles/r05/nt_exp/)
 #ifndef CTN_WS_NT
-#define CTN_WS_NT 0
+#define CTN_WS_NT 32
 #endif
 #ifndef CTN_WS_PRIO
 #define CTN_WS_PRIO 0
@@ -305,7 +307,7 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
     for (int j = 0; j < NA; ++j) {
       const int r = t * TM + rl0 + j * RSTEP;
       if constexpr (CTN_WS_EXP & 2) ra[s][j] = v4u{(uint32_t)r, 0u, 0u, 0u};
-      else ra[s][j] = ldg16(A + (size_t)r * p.lda + kc * 8);
+      else ra[s][j] = ldg16h<(CTN_WS_NT & 32) != 0 && N1B>(A + (size_t)r * p.lda + kc * 8);
       if constexpr (N1B) rh[s][j] = ldg16(H1 + (size_t)r * p.lda + kc * 8);
       if constexpr (CB) {
       } else if constexpr (OPK != OP_PLAIN && !FOLDS && (CTN_WS_EXP & 2048)) {
