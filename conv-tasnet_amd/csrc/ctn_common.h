@@ -71,7 +71,8 @@ CTN_DEV void stg16(void* p, v4u v) {
   if constexpr (CTN_NT & 2) __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(p));
   else *reinterpret_cast<v4u*>(p) = v;
 }
-// CTN_PART_NT: fp32 split-K partial sums of the dual and column GEMMs (read back only by
+// CTN_PART_NT (1 and 2: nontemporal; 2: 16-byte stores after a quad transpose of the
+// accumulators, instead of one dword per lane and row): fp32 split-K partial sums of the dual and column GEMMs (read back only by
 // the reductions at the end of the backward pass) stored with the nontemporal hint, so
 // they do not evict the activations the next kernels read from the Infinity Cache
 // (dw_bwd after the dual 85 -> 77 us, the dual itself +2.4, the column GEMM -1.5;
@@ -342,6 +343,26 @@ template <typename V> CTN_DEV V wave_sum_group(V v, int width) {
 // wave-uniform (read from lane 63).
 template <int CTRL, int ROW_MASK> CTN_DEV float dpp_f(float x) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, ROW_MASK, 0xF, false));
+}
+// 4x4 transpose within each quad of lanes (DPP quad_perm, no LDS): on entry lane t = lane & 3
+// holds v[e] = M[e][t], on exit v[c] = M[t][c].  Every lane of a quad must be active.
+CTN_DEV void quad_transpose4(float v[4]) {
+  const int t = (int)(threadIdx.x & 3);
+#pragma unroll
+  for (int e = 0; e < 4; e += 2) {   // partner t ^ 1 (quad_perm [1,0,3,2])
+    const float r = dpp_f<0xB1, 0xF>((t & 1) ? v[e] : v[e + 1]);
+    if (t & 1) v[e] = r;
+    else v[e + 1] = r;
+  }
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {      // partner t ^ 2 (quad_perm [2,3,0,1])
+    const float r = dpp_f<0x4E, 0xF>((t & 2) ? v[e] : v[e + 2]);
+    if (t & 2) v[e] = r;
+    else v[e + 2] = r;
+  }
+}
+CTN_DEV v4u f4bits(const float v[4]) {
+  return v4u{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
 }
 CTN_DEV float wave_sum_dpp(float v) {
   v += dpp_f<0xB1, 0xF>(v);    // quad_perm [1,0,3,2]

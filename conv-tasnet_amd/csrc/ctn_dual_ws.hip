@@ -681,9 +681,16 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
     for (int i = 0; i < CI; ++i)
 #pragma unroll
       for (int j = 0; j < CJ; ++j) {
-        const int n = n0 + (wn * CJ + j) * 16 + lr;
+        if constexpr (CTN_PART_NT == 2) {   // lane (lg, 4q + t): row 4lg + t, channels 4q .. 4q+3
+          float v[4] = {dacc[i][j][0], dacc[i][j][1], dacc[i][j][2], dacc[i][j][3]};
+          quad_transpose4(v);
+          const int n = n0 + (wn * CJ + j) * 16 + (lr & ~3);
+          stg16h<true>(&Dp[(size_t)((wp * CI + i) * 16 + 4 * lg + (lr & 3)) * p.Nout + n], f4bits(v));
+        } else {
+          const int n = n0 + (wn * CJ + j) * 16 + lr;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) st_part(&Dp[(size_t)((wp * CI + i) * 16 + 4 * lg + e) * p.Nout + n], dacc[i][j][e]);
+          for (int e = 0; e < 4; ++e) st_part(&Dp[(size_t)((wp * CI + i) * 16 + 4 * lg + e) * p.Nout + n], dacc[i][j][e]);
+        }
       }
     return;
   }

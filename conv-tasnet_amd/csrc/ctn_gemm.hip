@@ -718,12 +718,21 @@ __global__ __launch_bounds__(256 * ColsCks<T>::v) void gemm_cols_kernel(GemmCols
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int qq = q0 + wq * 64 + j * 16 + lr;
-      if (qq >= p.Q) continue;
+      if constexpr (CTN_PART_NT == 2) {   // lane (lg, 4q + t): row lg*4 + t, columns 4q .. 4q+3
+        const int qq = q0 + wq * 64 + j * 16 + (lr & ~3);
+        if (qq >= p.Q) continue;          // whole quads (Q % 8 == 0)
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        quad_transpose4(v);
+        const int pr = p0 + wp * 64 + i * 16 + lg * 4 + (lr & 3);
+        if (pr < p.P) stg16h<true>(&Cp[(size_t)pr * p.Q + qq], f4bits(v));
+      } else {
+        const int qq = q0 + wq * 64 + j * 16 + lr;
+        if (qq >= p.Q) continue;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int pr = p0 + wp * 64 + i * 16 + lg * 4 + e;
-        if (pr < p.P) st_part(&Cp[(size_t)pr * p.Q + qq], acc[i][j][e]);
+        for (int e = 0; e < 4; ++e) {
+          const int pr = p0 + wp * 64 + i * 16 + lg * 4 + e;
+          if (pr < p.P) st_part(&Cp[(size_t)pr * p.Q + qq], acc[i][j][e]);
+        }
       }
     }
 }
