@@ -66,6 +66,12 @@ CTN_DEV void unpack8(const v4u& v, float f[8]) { unpack_bf16x8(v, f); }
 #ifndef CTN_DW_NT
 #define CTN_DW_NT 3
 #endif
+// CTN_DW_NTL bits: the nontemporal hint on dw_bwd's d and dL/dn2 loads (1: their last use;
+// dw_bwd -2.8 us, gx after it -1.7, the next dual +2.4), on dw_fwd's h1 loads (2: dw_fwd
+// +6.4, off)
+#ifndef CTN_DW_NTL
+#define CTN_DW_NTL 1
+#endif
 template <bool NT = false>
 CTN_DEV void row_store(void* base, v4u v, int row) {
   stg16h<NT>(reinterpret_cast<char*>(base) + (size_t)row * 1024 + (threadIdx.x & 63) * 16u, v);
@@ -117,7 +123,9 @@ __global__ __launch_bounds__(256, 4) void dw_fwd_wave_kernel(DwArgs a) {
   }
   const int jK = steps_below(K, it.rho, dil);
   auto row_at = [&](int s) { return it.base + ((unsigned)s < (unsigned)jK ? it.rho + s * dil : 0); };
-  auto ld = [&](int row) { return __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rH, vo, row * (H * 2), 0)); };
+  auto ld = [&](int row) {
+    return __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rH, vo, row * (H * 2), (CTN_DW_NTL & 2) ? 2 : 0));
+  };
 
   // cLN statistics of the newest row, in batches of CB steps (as dw_bwd_wave_kernel)
   constexpr int CB = 63;
@@ -344,10 +352,14 @@ __global__ __launch_bounds__(256, 2) void dw_bwd_wave_kernel(DwArgs a) {
   // compiler sink one step's accumulations into the next step's blocks)
   auto row_at = [&](int s) { return it.base + ((unsigned)s < (unsigned)jK ? it.rho + s * dil : 0); };
   auto ld = [&](rsrc_t r, int row) { return __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, vo, row * (H * 2), 0)); };
+  // d and dL/dn2 are read here for the last time (CTN_DW_NTL bit 0: with the nontemporal hint)
+  auto ld_last = [&](rsrc_t r, int row) {
+    return __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, vo, row * (H * 2), (CTN_DW_NTL & 1) ? 2 : 0));
+  };
   auto load_row = [&](int j, BwdRow& r) __attribute__((always_inline)) {
     const int rg = row_at(j + GT);
-    r.d = ld(rD, rg);
-    r.g = ld(rG, rg);
+    r.d = ld_last(rD, rg);
+    r.g = ld_last(rG, rg);
     r.h = ld(rH, row_at(j));
   };
 
