@@ -69,6 +69,10 @@ CTN_DEV void unpack8(const v4u& v, float f[8]) { unpack_bf16x8(v, f); }
 // CTN_DW_NTL bits: the nontemporal hint on dw_bwd's d and dL/dn2 loads (1: their last use;
 // dw_bwd -2.8 us, gx after it -1.7, the next dual +2.4), on dw_fwd's h1 loads (2: dw_fwd
 // +6.4, off)
+// 1: dw_bwd's per-channel constants half-major in LDS (conflict-free reads); 0: lane-major
+#ifndef CTN_DW_CSTH
+#define CTN_DW_CSTH 1
+#endif
 #ifndef CTN_DW_NTL
 #define CTN_DW_NTL 1
 #endif
@@ -314,13 +318,18 @@ __global__ __launch_bounds__(256, 2) void dw_bwd_wave_kernel(DwArgs a) {
   // Per-channel constants (taps, gamma1, beta1, gamma2) live in LDS, read where they are
   // used: held in registers for the whole walk (48 per lane) they pushed the kernel past
   // the 256 registers of two waves per SIMD.
+  // Row r holds the two 4-channel halves of every lane's 8 channels half-major
+  // ([hf][lane][4]): one ds_read_b128 of a half then takes 16 consecutive bytes per lane,
+  // conflict-free in every lane group (lane-major, the lanes' 32-byte stride put two lanes
+  // of each group on one 16-byte slot: a 2-way conflict on every read of the walk).
   __shared__ __attribute__((aligned(16))) float cst[P + 3][H];   // w[0..P-1], gamma1, beta1, gamma2
   for (int i = threadIdx.x; i < H; i += 256) {
+    const int c = CTN_DW_CSTH ? ((i >> 2) & 1) * (H / 2) + (i >> 3) * 4 + (i & 3) : i;   // i = 8 lane + 4 hf + k
 #pragma unroll
-    for (int t = 0; t < P; ++t) cst[t][i] = a.wd[i * P + t];
-    cst[P][i] = a.gamma1[i];
-    cst[P + 1][i] = a.beta1[i];
-    cst[P + 2][i] = a.gamma2[i];
+    for (int t = 0; t < P; ++t) cst[t][c] = a.wd[i * P + t];
+    cst[P][c] = a.gamma1[i];
+    cst[P + 1][c] = a.beta1[i];
+    cst[P + 2][c] = a.gamma2[i];
   }
   __syncthreads();
   // LDS address of the lane's 8 channels; re-derived opaquely in every step so the loads
@@ -328,12 +337,12 @@ __global__ __launch_bounds__(256, 2) void dw_bwd_wave_kernel(DwArgs a) {
   // (the lane's LDS base is re-derived opaquely once per use site, cbase(), so the loads are
   // not hoisted out of the walk; the row / half offsets fold into the instructions' offsets)
   auto cbase = [&]() __attribute__((always_inline)) {
-    uint32_t b = lane * 32u;
+    uint32_t b = lane * (CTN_DW_CSTH ? 16u : 32u);
     asm volatile("" : "+v"(b));
     return b;
   };
   auto cvec4 = [&](uint32_t b, int r, int hf) __attribute__((always_inline)) {   // channels 8 lane + 4 hf ..
-    return *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(&cst[0][0]) + b + (r * H * 4 + hf * 16));
+    return *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(&cst[0][0]) + b + (r * H * 4 + hf * (CTN_DW_CSTH ? H * 2 : 16)));
   };
   auto f4 = [](const float4& v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; };
   float cgam[8], cbet[8], cgam2[8], cbet2[8], cwd[P][8];

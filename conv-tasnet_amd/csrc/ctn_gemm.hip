@@ -447,6 +447,9 @@ template <typename T> struct ColsCks { static constexpr int v = sizeof(T) == 2 ?
 #ifndef CTN_COLS_NTB
 #define CTN_COLS_NTB 0
 #endif
+#ifndef CTN_COLS_XLM
+#define CTN_COLS_XLM 0
+#endif
 #ifndef CTN_COLS_CKR
 #define CTN_COLS_CKR 32  // bf16 frame rows per k-step (experiment switch: 32 or 64)
 #endif
@@ -692,22 +695,26 @@ __global__ __launch_bounds__(256 * ColsCks<T>::v) void gemm_cols_kernel(GemmCols
   // groups 1.. hand their accumulators to group 0 through LDS (the stages are free
   // after this barrier), in group order: a fixed summation order
   __syncthreads();
+  // accumulator-major image: for accumulator a, the group's 256 lanes store 16 B each,
+  // consecutively (a lane-major image put every lane of a wave on the same four banks)
   float* xch = reinterpret_cast<float*>(smem_all);
-  const int xi = (wid * 64 + lane) * 64;   // 64 accumulators per lane, lane-major
+  static_assert(16 * 256 * 4 * sizeof(float) <= sizeof(smem_all), "exchange image fits the stages");
+  // (CTN_COLS_XLM=1: the old lane-major image, for A/B runs)
+  auto xi = [&](int a) { return CTN_COLS_XLM ? (tid * 16 + a) * 4 : (a * 256 + tid) * 4; };
   for (int g = 1; g < CKS; ++g) {
     if (grp == g) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          *reinterpret_cast<f32x4_t*>(&xch[xi + (i * 4 + j) * 4]) = acc[i][j];
+          *reinterpret_cast<f32x4_t*>(&xch[xi(i * 4 + j)]) = acc[i][j];
     }
     __syncthreads();
     if (grp == 0) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] += *reinterpret_cast<const f32x4_t*>(&xch[xi + (i * 4 + j) * 4]);
+        for (int j = 0; j < 4; ++j) acc[i][j] += *reinterpret_cast<const f32x4_t*>(&xch[xi(i * 4 + j)]);
     }
     __syncthreads();
   }
