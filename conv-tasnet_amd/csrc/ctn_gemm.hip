@@ -444,6 +444,9 @@ template <> CTN_DEV int cswz<float>(int row, int col) { return row * ColsPitch<f
 #endif
 template <typename T> struct ColsCks { static constexpr int v = sizeof(T) == 2 ? CTN_COLS_CKS : 2; };
 // 1 (experiment switch): the B-operand loads carry the nontemporal hint
+#ifndef CTN_COLS_NTA
+#define CTN_COLS_NTA 0   // 1 (experiment switch): the A-operand loads carry the nontemporal hint
+#endif
 #ifndef CTN_COLS_NTB
 #define CTN_COLS_NTB 0
 #endif
@@ -526,7 +529,7 @@ __global__ __launch_bounds__(256 * ColsCks<T>::v) void gemm_cols_kernel(GemmCols
       const int c = tid + 256 * i, rl = c / CPR;
       const int r = r0 + rl;
       // unconditional loads (clamped column; zeroed in swrite) keep the loop branch-free
-      R.a[i] = ldg16(A + (size_t)r * p.lda + (pin ? p0 + cc0 * E : 0));
+      R.a[i] = ldg16h<CTN_COLS_NTA != 0>(A + (size_t)r * p.lda + (pin ? p0 + cc0 * E : 0));
       R.b[i] = ldg16h<CTN_COLS_NTB != 0>(B + (size_t)r * p.ldb + (qin ? q0 + cc0 * E : 0));
       if constexpr (NK == NORM_CLN) {
         if constexpr (OPA != OP_PLAIN) R.sa[i] = *reinterpret_cast<const f32x2_t*>(p.aop.stats + r);

@@ -96,10 +96,11 @@ constexpr int WS_FOLD_MAX = 512;   // utterances whose gLN operand stats a workg
 // of the forward H -> B GEMM (norm-2 operand, residual epilogue), 4 = the output (h1)
 // stores of the forward B -> H GEMM, 8 = the dL/dh1 stores of the data-gradient GEMM
 // (norm-1-backward operand), 16 = that GEMM's output (gx) stores, 32 = that GEMM's
-// dL/da1 operand loads (its last use; measured -1.7 us, the others slower or flat:
-// profiles/r05/nt_exp/)
+// dL/da1 operand loads, 64 = its h1 loads (both their last use).  Bit 32 measured
+// -1.7 us, bit 64 -2 us in the column GEMM after it; the others slower or flat
+// (profiles/r05/nt_exp/)
 #ifndef CTN_WS_NT
-#define CTN_WS_NT 32
+#define CTN_WS_NT 96
 #endif
 #ifndef CTN_WS_PRIO
 #define CTN_WS_PRIO 0
@@ -308,7 +309,7 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
       const int r = t * TM + rl0 + j * RSTEP;
       if constexpr (CTN_WS_EXP & 2) ra[s][j] = v4u{(uint32_t)r, 0u, 0u, 0u};
       else ra[s][j] = ldg16h<(CTN_WS_NT & 32) != 0 && N1B>(A + (size_t)r * p.lda + kc * 8);
-      if constexpr (N1B) rh[s][j] = ldg16(H1 + (size_t)r * p.lda + kc * 8);
+      if constexpr (N1B) rh[s][j] = ldg16h<(CTN_WS_NT & 64) != 0>(H1 + (size_t)r * p.lda + kc * 8);
       if constexpr (CB) {
       } else if constexpr (OPK != OP_PLAIN && !FOLDS && (CTN_WS_EXP & 2048)) {
         ast[s][j] = make_float2(0.1f, 1.3f);   // timing only: no statistics loads
