@@ -96,7 +96,8 @@ constexpr int WS_FOLD_MAX = 512;   // utterances whose gLN operand stats a workg
 // of the forward H -> B GEMM (norm-2 operand, residual epilogue), 4 = the output (h1)
 // stores of the forward B -> H GEMM, 8 = the dL/dh1 stores of the data-gradient GEMM
 // (norm-1-backward operand), 16 = that GEMM's output (gx) stores, 32 = that GEMM's
-// dL/da1 operand loads, 64 = its h1 loads (both their last use).  Bit 32 measured
+// dL/da1 operand loads, 64 = its h1 loads (both their last use), 128 = the H -> B GEMM's d
+// loads, 256 = the residual loads (x in the H -> B GEMM, gy in the gx GEMM).  Bit 32 measured
 // -1.7 us, bit 64 -2 us in the column GEMM after it; the others slower or flat
 // (profiles/r05/nt_exp/)
 #ifndef CTN_WS_NT
@@ -308,7 +309,8 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
     for (int j = 0; j < NA; ++j) {
       const int r = t * TM + rl0 + j * RSTEP;
       if constexpr (CTN_WS_EXP & 2) ra[s][j] = v4u{(uint32_t)r, 0u, 0u, 0u};
-      else ra[s][j] = ldg16h<(CTN_WS_NT & 32) != 0 && N1B>(A + (size_t)r * p.lda + kc * 8);
+      else ra[s][j] = ldg16h<((CTN_WS_NT & 32) != 0 && N1B) || ((CTN_WS_NT & 128) != 0 && OPK == OP_PRELU_NORM)>(
+               A + (size_t)r * p.lda + kc * 8);
       if constexpr (N1B) rh[s][j] = ldg16h<(CTN_WS_NT & 64) != 0>(H1 + (size_t)r * p.lda + kc * 8);
       if constexpr (CB) {
       } else if constexpr (OPK != OP_PLAIN && !FOLDS && (CTN_WS_EXP & 2048)) {
@@ -417,7 +419,7 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
       if constexpr (HAS_R) {
         const size_t off = (size_t)r * p.ldr + colbase;
 #pragma unroll
-        for (int q = 0; q < Q; ++q) rn[mb][q] = ldg16(Rp + off + q * 8);
+        for (int q = 0; q < Q; ++q) rn[mb][q] = ldg16h<(CTN_WS_NT & 256) != 0>(Rp + off + q * 8);
       }
       if constexpr (EPI == EPI_NORM_BWD) est[mb] = p.stats[stat_index<NK>(r, Kp)];
     }
