@@ -71,12 +71,12 @@ CTN_DEV void stg16(void* p, v4u v) {
   if constexpr (CTN_NT & 2) __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(p));
   else *reinterpret_cast<v4u*>(p) = v;
 }
-// CTN_PART_NT (1 and 2: nontemporal; 2: 16-byte stores after a quad transpose of the
-// accumulators, instead of one dword per lane and row): fp32 split-K partial sums of the dual and column GEMMs (read back only by
-// the reductions at the end of the backward pass) stored with the nontemporal hint, so
-// they do not evict the activations the next kernels read from the Infinity Cache
-// (dw_bwd after the dual 85 -> 77 us, the dual itself +2.4, the column GEMM -1.5;
-// DESIGN.md §15)
+// CTN_PART_NT: the fp32 split-K partial sums of the dual and column GEMMs (read back only
+// by the reductions at the end of the backward pass) are stored with the nontemporal
+// hint, so they do not evict the activations the next kernels read from the Infinity
+// Cache (dw_bwd after the dual 85 -> 77 us, the dual itself +2.4, the column GEMM -1.5;
+// DESIGN.md §15).  1: one dword per lane and row; 2 (experiment, slower): 16-byte
+// stores after a quad transpose of the accumulators; 0: plain stores.
 #ifndef CTN_PART_NT
 #define CTN_PART_NT 1
 #endif
