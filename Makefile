@@ -121,3 +121,18 @@ build/var/lib$(VAR).so: $(VOBJ)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(VOBJ)
 varlib: build/var/lib$(VAR).so
 .PHONY: varlib
+
+# round 6: dual GEMM variants by -D flags: build/dv6_<name> from DV6_<name> (tools/gpu.sh mb)
+DV6_base :=
+DV6_prow := -DCTN_DV_PRIO=1
+DV6_pcol := -DCTN_DV_PRIO=4
+DV6_pmem := -DCTN_DV_PRIO=16
+DV6_pmem2 := -DCTN_DV_PRIO=32
+DV6_partnt0 := -DCTN_PART_NT=0
+DV6_clnc0 := -DCTN_DV_CLNC=0
+DV6_NAMES := base prow pcol pmem pmem2 partnt0 clnc0
+dv6: $(patsubst %,build/dv6_%,$(DV6_NAMES))
+build/dv6_%: tools/microbench/dual_ws_bench.hip $(PKG)/csrc/ctn_dual_ws.hip $(PKG)/csrc/ctn_gemm_dual.hip $(HDR)
+	@mkdir -p build
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -Iinclude $(DEVFLAGS) $(DV6_$*) $< -o $@
+.PHONY: dv6

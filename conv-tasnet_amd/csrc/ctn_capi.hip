@@ -7,6 +7,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -140,79 +141,96 @@ extern "C" int ctn_timer_read(double* total_ms, int* launches) {
 }
 
 // ---------------------------------------------------------------------------
-// device error word (ctn_common.h CTN_DEVERR_*): one per device, allocated and zeroed on
-// first use; a pinned host mirror is refreshed asynchronously at the end of every backward
-// pass (ctn_tblock_reduce_grads) and checked at the next one, so a kernel that hit an
-// error fails the call within a step without a device synchronisation on the fast path
+// device error word (ctn_common.h CTN_DEVERR_*): one per device, a zero-initialised
+// __device__ variable of this code object (each device loads its own copy), so getting it
+// needs no allocation and no memset: safe on the first launch even inside a stream or
+// graph capture.  The pointer is cached per device in an atomic, so launches take no lock.
+// A pinned host mirror is refreshed asynchronously at the end of every backward pass
+// (ctn_tblock_reduce_grads) and checked at the next one, so a kernel that hit an error
+// fails the call within a step without a device synchronisation on the fast path.
 // ---------------------------------------------------------------------------
+__device__ uint32_t ctn_err_words[64];   // [0] is the word; the rest pads it to its own line
+
 namespace {
 constexpr int MAX_DEV = 64;
 struct DevErr {
   std::mutex mu;
-  uint32_t* word[MAX_DEV] = {};
-  volatile uint32_t* mirror[MAX_DEV] = {};
+  std::atomic<uint32_t*> word[MAX_DEV] = {};
+  std::atomic<uint32_t*> mirror[MAX_DEV] = {};
 };
 DevErr g_deverr;
 
-int dev_err_slot(int* dev) {
-  if (hipGetDevice(dev) != hipSuccess || *dev < 0 || *dev >= MAX_DEV) return -1;
+uint32_t* dev_err_word(int* dev) {
+  if (hipGetDevice(dev) != hipSuccess || *dev < 0 || *dev >= MAX_DEV) return nullptr;
+  uint32_t* w = g_deverr.word[*dev].load(std::memory_order_acquire);
+  if (w) return w;
+  void* a = nullptr;
+  if (hipGetSymbolAddress(&a, HIP_SYMBOL(ctn_err_words)) != hipSuccess) return nullptr;
+  g_deverr.word[*dev].store((uint32_t*)a, std::memory_order_release);
+  return (uint32_t*)a;
+}
+
+// the pinned host mirror of a device's word (allocated on the first refresh or status
+// call, never on a kernel launch)
+volatile uint32_t* dev_err_mirror(int dev) {
+  uint32_t* h = g_deverr.mirror[dev].load(std::memory_order_acquire);
+  if (h) return h;
   std::lock_guard<std::mutex> lk(g_deverr.mu);
-  if (!g_deverr.word[*dev]) {
-    void* w = nullptr;
-    void* h = nullptr;
-    if (hipMalloc(&w, 256) != hipSuccess) return -1;
-    if (hipMemset(w, 0, 256) != hipSuccess || hipHostMalloc(&h, 256, hipHostMallocDefault) != hipSuccess) {
-      (void)hipFree(w);
-      return -1;
-    }
-    *(volatile uint32_t*)h = 0u;
-    g_deverr.mirror[*dev] = (volatile uint32_t*)h;
-    g_deverr.word[*dev] = (uint32_t*)w;
+  h = g_deverr.mirror[dev].load(std::memory_order_relaxed);
+  if (!h) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, 256, hipHostMallocDefault) != hipSuccess) return nullptr;
+    *(volatile uint32_t*)p = 0u;
+    h = (uint32_t*)p;
+    g_deverr.mirror[dev].store(h, std::memory_order_release);
   }
-  return 0;
+  return h;
 }
 
 const char* dev_err_text(uint32_t w) {
   if (w & CTN_DEVERR_SPIN)
     return "a generation-word wait of a wave-specialised kernel ran out of polls (CTN_DEVERR_SPIN): that launch's "
            "outputs are invalid";
-  if (w & CTN_DEVERR_ADAM_TABLE)
-    return "ctn_adam_step_dev ran past its bias-correction table (CTN_DEVERR_ADAM_TABLE): the parameters were not "
-           "updated";
   return "unknown device error bit";
 }
 
 // the mirror of earlier copies (no synchronisation): non-zero once an error has been seen
 int dev_err_check_async() {
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEV || !g_deverr.mirror[dev]) return CTN_OK;
-  const uint32_t w = *g_deverr.mirror[dev];
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEV) return CTN_OK;
+  const uint32_t* h = g_deverr.mirror[dev].load(std::memory_order_acquire);
+  if (!h) return CTN_OK;
+  const uint32_t w = *(const volatile uint32_t*)h;
   if (w) return fail(CTN_ERR_HIP, "device error word 0x%x: %s", w, dev_err_text(w));
   return CTN_OK;
 }
 
 hipError_t dev_err_refresh(hipStream_t s) {
   int dev = 0;
-  if (dev_err_slot(&dev)) return hipErrorOutOfMemory;
-  return hipMemcpyAsync((void*)g_deverr.mirror[dev], g_deverr.word[dev], 4, hipMemcpyDeviceToHost, s);
+  uint32_t* w = dev_err_word(&dev);
+  volatile uint32_t* h = w ? dev_err_mirror(dev) : nullptr;
+  if (!h) return hipErrorOutOfMemory;
+  return hipMemcpyAsync((void*)h, w, 4, hipMemcpyDeviceToHost, s);
 }
 }  // namespace
 
 uint32_t* ctn::device_error_word() {
   int dev = 0;
-  return dev_err_slot(&dev) ? nullptr : g_deverr.word[dev];
+  return dev_err_word(&dev);
 }
 
 extern "C" int ctn_device_status(void* stream, uint32_t* word, int clear) {
   int dev = 0;
-  if (dev_err_slot(&dev)) return fail(CTN_ERR_HIP, "device error word: allocation failed");
+  uint32_t* dw = dev_err_word(&dev);
+  volatile uint32_t* mirror = dw ? dev_err_mirror(dev) : nullptr;
+  if (!mirror) return fail(CTN_ERR_HIP, "device error word: unavailable");
   hipStream_t s = (hipStream_t)stream;
   uint32_t w = 0;
   CTN_HIP(hipStreamSynchronize(s));
-  CTN_HIP(hipMemcpy(&w, g_deverr.word[dev], 4, hipMemcpyDeviceToHost));
+  CTN_HIP(hipMemcpy(&w, dw, 4, hipMemcpyDeviceToHost));
   if (clear && w) {
-    CTN_HIP(hipMemset(g_deverr.word[dev], 0, 4));
-    *g_deverr.mirror[dev] = 0u;
+    CTN_HIP(hipMemset(dw, 0, 4));
+    *mirror = 0u;
   }
   if (word) *word = w;
   if (w) return fail(CTN_ERR_HIP, "device error word 0x%x: %s", w, dev_err_text(w));
@@ -1553,10 +1571,8 @@ extern "C" int ctn_adam_step(const ctn_opt_segment* segs, const ctn_opt_chunk* c
                              const ctn_adam_hparams* hp, void* stream) {
   if (!segs || !chunks || !hp || nchunks < 0 || hp->step < 1)
     return fail(CTN_ERR_ARG, "ctn_adam_step: bad arguments");
-  // bias corrections in double on the host, as torch.optim.Adam computes them
-  const double bc1 = 1.0 - pow((double)hp->beta1, (double)hp->step);
-  const double bc2 = 1.0 - pow((double)hp->beta2, (double)hp->step);
-  AdamArgs a{hp->beta1, hp->beta2, hp->eps, hp->weight_decay, (float)(hp->lr / bc1), (float)sqrt(bc2)};
+  // bias corrections of step hp->step in fp64 on the device (adam_bias, ctn_optim.hip)
+  AdamArgs a{hp->beta1, hp->beta2, hp->eps, hp->weight_decay, hp->lr, hp->step, nullptr, nullptr};
   CTN_HIP(launch_adam(reinterpret_cast<const OptSegment*>(segs), reinterpret_cast<const OptChunk*>(chunks), nchunks,
                       a, (hipStream_t)stream));
   return CTN_OK;
@@ -1569,26 +1585,13 @@ extern "C" int ctn_opt_write_segments(ctn_opt_segment* dst, const ctn_opt_segmen
   return CTN_OK;
 }
 
-extern "C" int ctn_adam_table(const ctn_adam_hparams* hp, int32_t count, float* table) {
-  if (!hp || count < 0 || (count > 0 && !table)) return fail(CTN_ERR_ARG, "ctn_adam_table: bad arguments");
-  for (int32_t i = 0; i < count; ++i) {   // ctn_adam_step's arithmetic for step i + 1
-    const double bc1 = 1.0 - pow((double)hp->beta1, (double)(i + 1));
-    const double bc2 = 1.0 - pow((double)hp->beta2, (double)(i + 1));
-    table[2 * i] = (float)(hp->lr / bc1);
-    table[2 * i + 1] = (float)sqrt(bc2);
-  }
-  return CTN_OK;
-}
-
 extern "C" int ctn_adam_step_dev(const ctn_opt_segment* segs, const ctn_opt_chunk* chunks, int nchunks,
-                                 const ctn_adam_hparams* hp, const float* table_dev, int32_t table_len,
-                                 int32_t* counter, void* stream) {
-  if (!segs || !chunks || !hp || nchunks < 0 || !table_dev || table_len < 1 || !counter)
+                                 const ctn_adam_hparams* hp, const float* lr_dev, int32_t* counter, void* stream) {
+  if (!segs || !chunks || !hp || nchunks < 0 || !counter)
     return fail(CTN_ERR_ARG, "ctn_adam_step_dev: bad arguments");
-  AdamArgs a{hp->beta1, hp->beta2, hp->eps, hp->weight_decay, 0.f, 1.f};
+  AdamArgs a{hp->beta1, hp->beta2, hp->eps, hp->weight_decay, hp->lr, 1, lr_dev, nullptr};
   CTN_HIP(launch_adam_dev(reinterpret_cast<const OptSegment*>(segs), reinterpret_cast<const OptChunk*>(chunks),
-                          nchunks, a, reinterpret_cast<const float2*>(table_dev), table_len, counter,
-                          ctn::device_error_word(), (hipStream_t)stream));
+                          nchunks, a, counter, (hipStream_t)stream));
   return CTN_OK;
 }
 
@@ -1975,25 +1978,50 @@ bool stream_graph_enabled() {
 struct StreamGraph {
   std::vector<uintptr_t> key;
   hipGraphExec_t exec;
+  hipEvent_t done;   // recorded after every launch of exec (launches of one exec are ordered)
 };
 std::mutex g_sg_mu;
 std::vector<StreamGraph> g_sg;   // most recently stored last; at most 8
-hipGraphExec_t stream_graph_find(const std::vector<uintptr_t>& key) {
-  std::lock_guard<std::mutex> lk(g_sg_mu);
-  for (const StreamGraph& g : g_sg)
-    if (g.key == key) return g.exec;
-  return nullptr;
-}
-void stream_graph_store(const std::vector<uintptr_t>& key, hipGraphExec_t exec) {
-  std::lock_guard<std::mutex> lk(g_sg_mu);
-  if (g_sg.size() == 8) {
-    // the evicted graph may still be running on some stream: let the device finish it
-    // first (rare: a ninth distinct argument set)
-    (void)hipDeviceSynchronize();
-    (void)hipGraphExecDestroy(g_sg.front().exec);
-    g_sg.erase(g_sg.begin());
+// Finds (or builds with `build`) the graph of `key` and launches it on s behind a
+// pos store, all under the cache lock, so no other thread can evict the graph between
+// the lookup and the launch.  An evicted graph is destroyed after the lock is released,
+// once its own last launch has finished (its event): no device-wide synchronisation,
+// nothing that would stall other streams or invalidate another thread's capture.
+template <typename Build>
+hipError_t stream_graph_launch(const std::vector<uintptr_t>& key, Build build, long* pos_dev, long pos, hipStream_t s) {
+  StreamGraph victim{{}, nullptr, nullptr};
+  hipError_t e = hipSuccess;
+  {
+    std::lock_guard<std::mutex> lk(g_sg_mu);
+    StreamGraph* g = nullptr;
+    for (StreamGraph& x : g_sg)
+      if (x.key == key) g = &x;
+    if (!g) {
+      hipGraphExec_t exec = nullptr;
+      hipEvent_t ev = nullptr;
+      e = build(&exec);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+      if (e != hipSuccess) {
+        if (exec) (void)hipGraphExecDestroy(exec);
+        return e;
+      }
+      if (g_sg.size() == 8) {
+        victim = g_sg.front();
+        g_sg.erase(g_sg.begin());
+      }
+      g_sg.push_back(StreamGraph{key, exec, ev});
+      g = &g_sg.back();
+    }
+    e = launch_stream_set_pos(pos_dev, pos, s);
+    if (e == hipSuccess) e = hipGraphLaunch(g->exec, s);
+    if (e == hipSuccess) e = hipEventRecord(g->done, s);
   }
-  g_sg.push_back(StreamGraph{key, exec});
+  if (victim.exec) {   // a ninth distinct argument set (rare)
+    (void)hipEventSynchronize(victim.done);
+    (void)hipGraphExecDestroy(victim.exec);
+    (void)hipEventDestroy(victim.done);
+  }
+  return e;
 }
 }  // namespace
 
@@ -2084,24 +2112,22 @@ extern "C" int ctn_stream_call(const ctn_stream_desc* d, const ctn_stream_model*
                           (const void*)b.w2_t, (const void*)b.ring})
       key.push_back((uintptr_t)v);
   }
-  hipGraphExec_t exec = stream_graph_find(key);
-  if (!exec) {
+  auto build = [&](hipGraphExec_t* exec) -> hipError_t {
     hipStream_t cs = nullptr;
-    CTN_HIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    hipError_t e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking);
+    if (e != hipSuccess) return e;
     hipGraph_t g = nullptr;
-    hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
+    e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
     if (e == hipSuccess) {
       const hipError_t el = enqueue(cs, pos_dev);
       e = hipStreamEndCapture(cs, &g);
       if (el != hipSuccess) e = el;
     }
-    if (e == hipSuccess) e = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0);
+    if (e == hipSuccess) e = hipGraphInstantiate(exec, g, nullptr, nullptr, 0);
     if (g) (void)hipGraphDestroy(g);
     (void)hipStreamDestroy(cs);
-    CTN_HIP(e);
-    stream_graph_store(key, exec);
-  }
-  CTN_HIP(launch_stream_set_pos(pos_dev, (long)pos, s));
-  CTN_HIP(hipGraphLaunch(exec, s));
+    return e;
+  };
+  CTN_HIP(stream_graph_launch(key, build, pos_dev, (long)pos, s));
   return CTN_OK;
 }

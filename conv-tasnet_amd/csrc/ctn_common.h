@@ -133,9 +133,6 @@ CTN_DEV void lds_barrier() {
 #ifndef CTN_SPIN_LIMIT
 #define CTN_SPIN_LIMIT (1u << 22)
 #endif
-#ifndef CTN_DEVERR_ADAM_TABLE
-#define CTN_DEVERR_ADAM_TABLE 2u   // ctn_adam_step_dev past its table (include/ctn.h)
-#endif
 #ifndef CTN_DEVERR_SPIN
 #define CTN_DEVERR_SPIN 1u   // a generation-word wait timed out (include/ctn.h)
 #endif

@@ -309,15 +309,23 @@ struct OptChunk { int32_t seg; uint32_t len; int64_t off; };
 constexpr int OPT_CHUNK = 8192;                 // elements per workgroup
 constexpr uint32_t OPT_UNALIGNED = 0x80000000u;  // len flag: scalar path
 constexpr uint32_t OPT_LEN_MASK = 0x7fffffffu;
-struct AdamArgs { float b1, b2, eps, wd, step_size, bc2_sqrt; };
+// Bias corrections on the device in fp64 from the step count (ABI v12): step t = *counter + 1
+// when counter is set (graph capture), else `step`; lr from *lr_dev when set, else `lr`
+struct AdamArgs {
+  float b1, b2, eps, wd, lr;
+  int step;
+  const float* lr_dev;
+  const int* counter;
+};
 hipError_t launch_grad_sqnorm(const OptSegment* segs, const OptChunk* chunks, int nchunks, float* partial,
                               hipStream_t s);
 hipError_t launch_grad_clip(const OptSegment* segs, const OptChunk* chunks, int nchunks, const float* partial,
                             float max_norm, float* total_norm, hipStream_t s);
 hipError_t launch_adam(const OptSegment* segs, const OptChunk* chunks, int nchunks, const AdamArgs& a,
                        hipStream_t s);
+// the same update with a.counter set, then a one-lane kernel increments *counter
 hipError_t launch_adam_dev(const OptSegment* segs, const OptChunk* chunks, int nchunks, const AdamArgs& a,
-                           const float2* table, int table_len, int* counter, uint32_t* err, hipStream_t s);
+                           int* counter, hipStream_t s);
 hipError_t launch_write_segments(OptSegment* dst, const OptSegment* src, int n, hipStream_t s);
 
 // ---- streaming causal separation (ctn_stream.hip) ----------------------------------

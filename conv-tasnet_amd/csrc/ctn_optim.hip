@@ -87,16 +87,30 @@ __global__ __launch_bounds__(OPT_THREADS) void grad_clip_kernel(const OptSegment
 // torch.optim.Adam (amsgrad=False, maximize=False), per element:
 //   g += wd * p;  m = lerp(m, g, 1-b1);  v = b2 v + (1-b2) g^2
 //   p -= step_size * m / (sqrt(v) / bc2_sqrt + eps),  step_size = lr / (1 - b1^t)
-CTN_DEV void adam_elem(float& p, float g, float& m, float& v, const AdamArgs& a) {
+struct AdamStep { float step_size, bc2_sqrt; };
+CTN_DEV void adam_elem(float& p, float g, float& m, float& v, const AdamArgs& a, const AdamStep& k) {
   g = a.wd != 0.f ? fmaf(a.wd, p, g) : g;
   m = fmaf(1.f - a.b1, g - m, m);   // exp_avg.lerp_(grad, 1 - beta1)
   v = fmaf(a.b2, v, (1.f - a.b2) * g * g);
-  const float den = sqrtf(v) / a.bc2_sqrt + a.eps;
-  p = p - a.step_size * (m / den);
+  const float den = sqrtf(v) / k.bc2_sqrt + a.eps;
+  p = p - k.step_size * (m / den);
+}
+
+// torch's bias corrections (torch.optim.Adam, non-capturable: Python doubles) for step t:
+// step_size = lr / (1 - b1^t), bc2_sqrt = sqrt(1 - b2^t), in fp64 on the device, for the
+// eager and the capturable launch alike (so both give the same bits at every step, and the
+// capturable one has no step limit: t is the device counter + 1)
+CTN_DEV AdamStep adam_bias(const AdamArgs& a) {
+  const int t = a.counter ? *a.counter + 1 : a.step;
+  const double lr = a.lr_dev ? (double)*a.lr_dev : (double)a.lr;
+  const double bc1 = 1.0 - pow((double)a.b1, (double)t);
+  const double bc2 = 1.0 - pow((double)a.b2, (double)t);
+  return AdamStep{(float)(lr / bc1), (float)sqrt(bc2)};
 }
 
 __global__ __launch_bounds__(OPT_THREADS) void adam_kernel(const OptSegment* segs, const OptChunk* chunks,
                                                            AdamArgs a) {
+  const AdamStep k = adam_bias(a);
   int si, len; long off; bool vec;
   opt_chunk(chunks, si, off, len, vec);
   const OptSegment s = segs[si];
@@ -112,61 +126,17 @@ __global__ __launch_bounds__(OPT_THREADS) void adam_kernel(const OptSegment* seg
       const float4 G = reinterpret_cast<const float4*>(g)[i];
       float4 Mv = reinterpret_cast<float4*>(m)[i];
       float4 V = reinterpret_cast<float4*>(v)[i];
-      adam_elem(P.x, G.x, Mv.x, V.x, a);
-      adam_elem(P.y, G.y, Mv.y, V.y, a);
-      adam_elem(P.z, G.z, Mv.z, V.z, a);
-      adam_elem(P.w, G.w, Mv.w, V.w, a);
+      adam_elem(P.x, G.x, Mv.x, V.x, a, k);
+      adam_elem(P.y, G.y, Mv.y, V.y, a, k);
+      adam_elem(P.z, G.z, Mv.z, V.z, a, k);
+      adam_elem(P.w, G.w, Mv.w, V.w, a, k);
       reinterpret_cast<float4*>(p)[i] = P;
       reinterpret_cast<float4*>(m)[i] = Mv;
       reinterpret_cast<float4*>(v)[i] = V;
     }
     done = n4 << 2;
   }
-  for (int i = done + threadIdx.x; i < len; i += OPT_THREADS) adam_elem(p[i], g[i], m[i], v[i], a);
-}
-
-// Graph-capturable Adam (ABI v10): the step count lives in device memory and the bias
-// corrections of step t come from a host-computed table (the same double arithmetic as
-// ctn_adam_step, so the same bits), so a captured step replays correctly; a bump kernel
-// advances the count after the update.  t past the table sets CTN_DEVERR_ADAM_TABLE and
-// leaves the parameters untouched.
-__global__ __launch_bounds__(OPT_THREADS) void adam_dev_kernel(const OptSegment* segs, const OptChunk* chunks,
-                                                               AdamArgs a, const float2* table, int table_len,
-                                                               const int* counter, uint32_t* err) {
-  const int t = *counter + 1;
-  if (t < 1 || t > table_len) {
-    if (blockIdx.x == 0 && threadIdx.x == 0 && err) atomicOr(err, (uint32_t)CTN_DEVERR_ADAM_TABLE);
-    return;
-  }
-  const float2 bc = table[t - 1];
-  a.step_size = bc.x;
-  a.bc2_sqrt = bc.y;
-  int si, len; long off; bool vec;
-  opt_chunk(chunks, si, off, len, vec);
-  const OptSegment s = segs[si];
-  float* p = s.p + off;
-  const float* g = s.g + off;
-  float* m = s.m + off;
-  float* v = s.v + off;
-  int done = 0;
-  if (vec) {
-    const int n4 = len >> 2;
-    for (int i = threadIdx.x; i < n4; i += OPT_THREADS) {
-      float4 P = reinterpret_cast<float4*>(p)[i];
-      const float4 G = reinterpret_cast<const float4*>(g)[i];
-      float4 Mv = reinterpret_cast<float4*>(m)[i];
-      float4 V = reinterpret_cast<float4*>(v)[i];
-      adam_elem(P.x, G.x, Mv.x, V.x, a);
-      adam_elem(P.y, G.y, Mv.y, V.y, a);
-      adam_elem(P.z, G.z, Mv.z, V.z, a);
-      adam_elem(P.w, G.w, Mv.w, V.w, a);
-      reinterpret_cast<float4*>(p)[i] = P;
-      reinterpret_cast<float4*>(m)[i] = Mv;
-      reinterpret_cast<float4*>(v)[i] = V;
-    }
-    done = n4 << 2;
-  }
-  for (int i = done + threadIdx.x; i < len; i += OPT_THREADS) adam_elem(p[i], g[i], m[i], v[i], a);
+  for (int i = done + threadIdx.x; i < len; i += OPT_THREADS) adam_elem(p[i], g[i], m[i], v[i], a, k);
 }
 
 __global__ void adam_bump_kernel(int* counter) {
@@ -196,11 +166,11 @@ hipError_t launch_write_segments(OptSegment* dst, const OptSegment* src, int n, 
 }
 
 hipError_t launch_adam_dev(const OptSegment* segs, const OptChunk* chunks, int nchunks, const AdamArgs& a,
-                           const float2* table, int table_len, int* counter, uint32_t* err, hipStream_t s) {
-  if (!segs || !chunks || nchunks < 0 || !table || table_len < 1 || !counter) return hipErrorInvalidValue;
-  if (nchunks > 0)
-    hipLaunchKernelGGL(adam_dev_kernel, dim3(nchunks), dim3(OPT_THREADS), 0, s, segs, chunks, a, table, table_len,
-                       counter, err);
+                           int* counter, hipStream_t s) {
+  if (!segs || !chunks || nchunks < 0 || !counter) return hipErrorInvalidValue;
+  AdamArgs ac = a;
+  ac.counter = counter;
+  if (nchunks > 0) hipLaunchKernelGGL(adam_kernel, dim3(nchunks), dim3(OPT_THREADS), 0, s, segs, chunks, ac);
   hipLaunchKernelGGL(adam_bump_kernel, dim3(1), dim3(64), 0, s, counter);
   return hipGetLastError();
 }

@@ -28,7 +28,20 @@ of the whole buffer after backward.
 
 Averaging matches DDP's: every gradient is divided by the world size, then summed
 across ranks (exact for power-of-two world sizes), so both give the same bits.
+
+An early chunk is all-reduced out of place (a scaled copy of the slice), so the views
+keep this rank's local gradients until :meth:`sync` copies the reduced values in.  A
+second backward pass before ``sync()`` (gradient accumulation, or a step abandoned
+without ``sync()``) therefore finds its views untouched by RCCL: the pass waits for the
+early chunks, drops them and turns the overlap off until the next ``sync()``, which
+all-reduces the whole buffer once (ctn_ops calls :meth:`on_pass_start`).
+
+The learnt layout decides the sequence of all-reduces every rank issues, so after it is
+learnt the ranks compare it (a hash of every chunk's parameter list, one all-reduce)
+and all raise if any rank learnt another one, instead of deadlocking in RCCL.
 """
+import hashlib
+
 import torch
 import torch.distributed as dist
 from torch._utils import _flatten_dense_tensors, _unflatten_dense_tensors
@@ -65,7 +78,9 @@ class FlatGradAllReduce:
         self._layout(self._buckets(self.params), None)
         self._reported = []     # this step's hook reports (lists of parameters), in order
         self._final = set()     # ids of parameters final in their views this step
-        self._launched = {}     # (arena, chunk) -> async all-reduce work
+        self._launched = {}     # (arena, chunk) -> (async all-reduce work, reduced copy, view slice)
+        self._passes = 0        # backward passes since the last sync()
+        self._accumulating = False   # a second pass before sync(): no early chunks this step
         self._learnt = False
         self.early_chunks = 0   # chunks all-reduced during a backward pass (overlapped)
         self._hook_devs = []
@@ -107,9 +122,26 @@ class FlatGradAllReduce:
         return list(by.values())
 
     # ---- ctn_ops exchange hook (called from the backward pass, in block order)
+    def on_pass_start(self):
+        """A backward pass begins (ctn_ops: the pass's first TemporalBlock backward).  If an
+        earlier pass since the last sync() already ran (gradient accumulation, or a step
+        abandoned without sync()), its early chunks are waited for and dropped — their views
+        still hold the local gradients — and this step exchanges everything in sync()."""
+        self._passes += 1
+        if self._passes > 1:
+            self._drop_early()
+            self._accumulating = True
+
+    def _drop_early(self):
+        for work, _, _ in self._launched.values():
+            work.wait()               # RCCL is done with the reduced copies before they are freed
+        self._launched, self._final, self._reported = {}, set(), []
+
     def on_reduced(self, params):
         """A group of deferred blocks' gradients is final, in place in their views: launch
         every chunk, in order, whose parameters are all final."""
+        if self._accumulating:
+            return
         self._reported.append(list(params))
         self._final.update(id(p) for p in params)
         if self._learnt:
@@ -122,12 +154,16 @@ class FlatGradAllReduce:
                     continue
                 if final_only and not all(id(p) in self._final for p in g[a:b]):
                     return            # in order: every rank issues the same sequence
-                if not final_only:
-                    self._gather(g[a:b], vs[a:b])
                 part = flat[o0:o1]
-                part.div_(self.world)
-                self._launched[(ai, ci)] = dist.all_reduce(part, group=self.group, async_op=True)
-                self.early_chunks += final_only
+                if final_only:
+                    # out of place: the views keep the local gradients until sync()
+                    red = part / self.world
+                    self._launched[(ai, ci)] = (dist.all_reduce(red, group=self.group, async_op=True), red, part)
+                    self.early_chunks += 1
+                else:
+                    self._gather(g[a:b], vs[a:b])
+                    part.div_(self.world)
+                    self._launched[(ai, ci)] = (dist.all_reduce(part, group=self.group, async_op=True), None, None)
 
     @staticmethod
     def _gather(params, views):
@@ -148,14 +184,19 @@ class FlatGradAllReduce:
         buffer (as DDP's gradient_as_bucket_view makes them): keep a copy, not the tensor,
         to hold a gradient past the next step."""
         self._launch(final_only=False)
-        for w in self._launched.values():
-            w.wait()                 # the current stream waits for RCCL's
+        for work, red, part in self._launched.values():
+            work.wait()              # the current stream waits for RCCL's
+            if red is not None:      # an early chunk, reduced out of place
+                part.copy_(red)
         for g, flat, vs, _ in self._arenas:
             for p, v in zip(g, vs):
                 p.grad = v
-        if not self._learnt and self._hook_devs:
+        # learnt collectively at the first sync() after a single-pass step (the layout check
+        # is an all-reduce every rank joins: CUDA buckets always learn, whatever they reported)
+        if not self._learnt and not self._accumulating and self.chunks > 1 and (self._hook_devs or self._reported):
             self._learn()
         self._reported, self._final, self._launched = [], set(), {}
+        self._passes, self._accumulating = 0, False
 
     def _learn(self):
         """After the first step: the blocks the hook reported, in report order, in
@@ -164,6 +205,7 @@ class FlatGradAllReduce:
         self._learnt = True
         if len(blocks) < 2:
             self.group_blocks = 1 << 30   # nothing to overlap: one exchange after backward
+            self._check_layout()
             return
         per = -(-len(blocks) // (self.chunks - 1))
         self.group_blocks = per
@@ -182,3 +224,27 @@ class FlatGradAllReduce:
                 bounds.setdefault(key, []).append((a, len(buckets[key])))
         keys = list(buckets)
         self._layout([buckets[k] for k in keys], [bounds[k] for k in keys])
+        self._check_layout()
+
+    def layout_signature(self):
+        """A hash of the learnt layout: every chunk's parameters (as indices into the
+        constructor's list), in the order the chunks are all-reduced."""
+        idx = {id(p): i for i, p in enumerate(self.params)}
+        desc = [(ai, [idx[id(p)] for p in g[a:b]]) for ai, (g, _, _, chunks) in enumerate(self._arenas)
+                for a, b, _, _ in chunks]
+        return int.from_bytes(hashlib.sha1(repr(desc).encode()).digest()[:8], "little", signed=True)
+
+    def _check_layout(self):
+        """Every rank must issue the same all-reduce sequence: compare the layout hashes
+        (max of h and of -h over the ranks: equal iff every rank holds the same h) and
+        raise on every rank if they differ, instead of deadlocking in RCCL later."""
+        h = self.layout_signature()
+        t = torch.tensor([h, -h], dtype=torch.int64, device=self.params[0].device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        hi, lo = int(t[0]), -int(t[1])
+        if hi != h or lo != h:
+            raise RuntimeError(
+                "FlatGradAllReduce: the ranks learnt different gradient-chunk layouts in the first "
+                f"step (this rank {h:#x}, max {hi:#x}, min {lo:#x}); their all-reduce sequences would "
+                "not match.  Every rank must run the same model with the same deferred TemporalBlock "
+                "backwards in its first step (or use chunks=1).")

@@ -14,7 +14,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CTN_HIP_LIB", os.path.join(_HERE, "libctn_hip.so"))
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 DTYPE_F32, DTYPE_BF16 = 0, 1
 NORM_GLN, NORM_CLN, NORM_BN = 0, 1, 2
@@ -143,9 +143,7 @@ _SIGS = {
                                           c_void_p]),
     "ctn_adam_step": (ctypes.c_int, [c_void_p, c_void_p, ctypes.c_int, c_void_p, c_void_p]),
     "ctn_opt_write_segments": (ctypes.c_int, [c_void_p, c_void_p, ctypes.c_int, c_void_p]),
-    "ctn_adam_table": (ctypes.c_int, [c_void_p, ctypes.c_int32, c_void_p]),
-    "ctn_adam_step_dev": (ctypes.c_int, [c_void_p, c_void_p, ctypes.c_int, c_void_p, c_void_p, ctypes.c_int32,
-                                         c_void_p, c_void_p]),
+    "ctn_adam_step_dev": (ctypes.c_int, [c_void_p, c_void_p, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "ctn_layernorm_workspace_bytes": (c_size_t, [c_void_p, ctypes.c_int, ctypes.c_int]),
     "ctn_layernorm_forward": (ctypes.c_int, [c_void_p, ctypes.c_int] + [c_void_p] * 5 + [c_void_p, c_size_t,
                                                                                        c_void_p]),

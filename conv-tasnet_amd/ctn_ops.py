@@ -287,10 +287,14 @@ def _task_state(dev) -> "_TaskState":
         # it ends after this one) or a pass that raised before its end (top-level: drop it;
         # its callback never ran).  The stack walk runs only in that rare case.
         others = [k for k in _TASKS if k[0] == dev]
-        if others and not _nested_backward():
+        nested = bool(others) and _nested_backward()
+        if others and not nested:
             for k in others:
                 del _TASKS[k]
         st = _TASKS[key] = _TaskState()
+        hook = _EXCHANGE_HOOKS.get(dev)
+        if hook is not None and not nested:
+            hook.on_pass_start()   # a second pass before the exchange's sync(): no early chunks
         torch.autograd.Variable._execution_engine.queue_callback(lambda: _end_of_backward(key))
     return st
 

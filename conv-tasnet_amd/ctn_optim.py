@@ -247,29 +247,32 @@ class Adam(torch.optim.Optimizer):
 
     # --- graph capture (torch.optim.Adam(capturable=True) semantics): the step count of a
     # capturable group lives in a device counter that the update kernel reads and a second
-    # kernel advances, and the bias corrections come from a device table built for the
-    # group's lr and betas (ctn_adam_table: ctn_adam_step's arithmetic, the same bits), so a
-    # captured step replays with the right step count.
-    TABLE_STEPS = 1 << 20
-
+    # kernel advances, and lr in a one-element device tensor; the bias corrections are
+    # computed from them on the device in fp64 (ctn_adam_step_dev: the same code as the
+    # eager ctn_adam_step, so the same bits), so a captured step replays as the next step,
+    # with no step limit.  A schedule that changes lr between replays writes
+    # ``lr_tensor(group_index)`` (outside the graph); an eager step refreshes it from the
+    # group's lr.
     def _capture_state(self, gi, group, dev, completed: int):
         c = self._cap.get(gi)
         if c is None:
             c = self._cap[gi] = {"counter": torch.full((1,), completed, dtype=torch.int32, device=dev),
-                                 "table": torch.empty(2 * self.TABLE_STEPS, dtype=torch.float32, device=dev),
-                                 "key": None}
-        b1, b2 = group["betas"]
-        key = (float(group["lr"]), float(b1), float(b2))
-        if c["key"] != key:
+                                 "lr": torch.full((1,), float(group["lr"]), dtype=torch.float32, device=dev),
+                                 "lr_host": float(group["lr"])}
+        if c["lr_host"] != float(group["lr"]):
             if torch.cuda.is_current_stream_capturing():
-                raise L.CtnLibraryError("Adam(capturable=True): lr or betas changed inside a graph capture; "
-                                        "step once eagerly after changing them, then capture")
-            host = np.empty(2 * self.TABLE_STEPS, dtype=np.float32)
-            hp = L.AdamHParams(key[0], key[1], key[2], 0.0, 0.0, 1)
-            L.check(L.load().ctn_adam_table(ctypes.byref(hp), self.TABLE_STEPS, host.ctypes.data), "ctn_adam_table")
-            c["table"].copy_(torch.from_numpy(host))
-            c["key"] = key
+                raise L.CtnLibraryError("Adam(capturable=True): lr changed inside a graph capture; write "
+                                        "lr_tensor(group) outside the graph instead")
+            c["lr"].fill_(float(group["lr"]))
+            c["lr_host"] = float(group["lr"])
         return c
+
+    def lr_tensor(self, group_index: int = 0) -> torch.Tensor:
+        """The device lr of a capturable group (what replays of a captured step read)."""
+        c = self._cap.get(group_index)
+        if c is None:
+            raise L.CtnLibraryError("lr_tensor: the group has not stepped as capturable yet")
+        return c["lr"]
 
     def _launch(self, lib, gi, group, dev, segs_dev, plan, n: int):
         """Step n (1-based) of a group: ctn_adam_step, or for a capturable group
@@ -283,8 +286,8 @@ class Adam(torch.optim.Optimizer):
             return
         c = self._capture_state(gi, group, dev, n - 1)
         L.check(lib.ctn_adam_step_dev(segs_dev.data_ptr(), plan.chunks.data_ptr(), plan.nchunks, ctypes.byref(hp),
-                                      c["table"].data_ptr(), self.TABLE_STEPS, c["counter"].data_ptr(),
-                                      L.stream_handle(dev)), "ctn_adam_step_dev")
+                                      c["lr"].data_ptr(), c["counter"].data_ptr(), L.stream_handle(dev)),
+                "ctn_adam_step_dev")
 
     def zero_grad(self, set_to_none: bool = True):
         """torch.optim.Optimizer.zero_grad without its per-call profiler scope and

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define CTN_ABI_VERSION 11
+#define CTN_ABI_VERSION 12
 
 typedef enum { CTN_DTYPE_F32 = 0, CTN_DTYPE_BF16 = 1 } ctn_dtype;
 /* CTN_NORM_BN: torch.nn.BatchNorm1d, chose_norm's fallback branch (conv_tasnet.py:302-303) */
@@ -252,7 +252,8 @@ int ctn_opt_plan(const ctn_opt_segment* segs, int nseg, ctn_opt_chunk* chunks, i
  * segs/chunks: device tables; partial: device scratch of nchunks floats. */
 int ctn_grad_clip_norm(const ctn_opt_segment* segs, const ctn_opt_chunk* chunks, int nchunks, float max_norm,
                        float* total_norm, float* partial, void* stream);
-/* one Adam step of every segment (param, exp_avg, exp_avg_sq updated in place) */
+/* one Adam step of every segment (param, exp_avg, exp_avg_sq updated in place); the bias
+ * corrections of step hp->step are computed on the device in fp64 (ABI v12) */
 int ctn_adam_step(const ctn_opt_segment* segs, const ctn_opt_chunk* chunks, int nchunks, const ctn_adam_hparams* hp,
                   void* stream);
 
@@ -261,18 +262,16 @@ int ctn_adam_step(const ctn_opt_segment* segs, const ctn_opt_chunk* chunks, int 
  * launch time from the device, so a captured launch replays correctly:
  *  - ctn_opt_write_segments: writes n segment entries to the device table `dst` with
  *    kernels whose arguments carry the entries (no host staging buffer);
- *  - ctn_adam_table (host only): table[2*i], table[2*i+1] = the step size lr / (1 -
- *    beta1^t) and sqrt(1 - beta2^t) of step t = i + 1, for i < count, computed exactly as
- *    ctn_adam_step does (so both give the same bits); copy it to the device once per lr;
- *  - ctn_adam_step_dev: Adam with the step count in device memory: step t = *counter + 1
- *    reads table_dev[t - 1]; a second kernel then increments *counter.  t past table_len
- *    sets CTN_DEVERR_ADAM_TABLE in the device error word and updates nothing.
- * hp->lr and hp->step are not read by ctn_adam_step_dev (they are in the table). */
+ *  - ctn_adam_step_dev (ABI v12): Adam with the step count in device memory: step
+ *    t = *counter + 1, then a second kernel increments *counter; lr = *lr_dev when lr_dev
+ *    is not NULL (a schedule writes it between replays), else hp->lr.  The bias
+ *    corrections lr / (1 - beta1^t) and sqrt(1 - beta2^t) are computed on the device in
+ *    fp64 by the same code as ctn_adam_step's (same bits for the same t and lr), with no
+ *    step limit (ABI v10-11 read them from a host-built table of 2^20 steps).
+ * hp->step is not read by ctn_adam_step_dev. */
 int ctn_opt_write_segments(ctn_opt_segment* dst, const ctn_opt_segment* src, int n, void* stream);
-int ctn_adam_table(const ctn_adam_hparams* hp, int32_t count, float* table);
 int ctn_adam_step_dev(const ctn_opt_segment* segs, const ctn_opt_chunk* chunks, int nchunks,
-                      const ctn_adam_hparams* hp, const float* table_dev, int32_t table_len, int32_t* counter,
-                      void* stream);
+                      const ctn_adam_hparams* hp, const float* lr_dev, int32_t* counter, void* stream);
 
 /* -------------------------------------------------------------------------
  * Stand-alone separator layers on frame rows [M*Kp][C] (ABI v4): what the fused
@@ -451,7 +450,6 @@ int ctn_copy_bytes(void* dst, const void* src, size_t bytes, int workgroups, int
  * it is non-zero; clear != 0 resets it.
  * ------------------------------------------------------------------------- */
 #define CTN_DEVERR_SPIN 1u
-#define CTN_DEVERR_ADAM_TABLE 2u   /* ctn_adam_step_dev: step count past its table (ABI v10) */
 int ctn_device_status(void* stream, uint32_t* word, int clear);
 
 #ifdef __cplusplus

@@ -198,15 +198,39 @@ def test_model_bench_step_bf16_vs_oracle():
     assert float(dsnr.median()) < 0.05 and float(dsnr.max()) < 0.25, dsnr
     for b in (0, M // 2, M - 1):
         assert rel(est_m[b].detach().cpu(), est_r[b]) < 5e-2, b
-    pg = dict(model.named_parameters())
-    for n, shape in O.param_shapes(cfg):
+    _check_grads_bf16(cfg, dict(model.named_parameters()), grads_r, w_lim=0.1, n_lim=0.25, a_lim=0.3)
+
+
+def _check_grads_bf16(cfg, pg, grads_r, w_lim, n_lim, a_lim):
+    """Every parameter gradient TENSOR on its own against the oracle's (a permuted or
+    misplaced gradient of equal norm fails):
+      * conv / linear weights: relative L2 < w_lim;
+      * norm gamma / beta [1, C, 1]: relative L2 < n_lim (each entry a sum over one
+        channel's frames: fewer terms than a weight row, so more bf16 noise);
+      * PReLU alphas (one sum over every position of a block's [M, H, K] tensor, whose
+        terms cancel): |error| < a_lim x the mean |gradient| of all alphas, the bound of
+        test_gpu_model.py::test_bn_bf16_training_step."""
+    shapes = O.param_shapes(cfg)
+    alphas = [n for n, shape in shapes if shape == (1,)]
+    a_scale = float(np.mean([abs(float(grads_r[n].reshape(-1)[0])) for n in alphas]))
+    errs, bad = {}, []
+    for n, shape in shapes:
+        g, gr = pg[n].grad.detach().cpu().reshape(grads_r[n].shape).double(), grads_r[n].double()
+        assert torch.isfinite(g).all(), n
         if shape == (1,):
-            continue   # PReLU alpha in bf16: cancellation-heavy scalar (see test_gpu_tblock.py)
-        g, gr = pg[n].grad.detach().cpu().reshape(grads_r[n].shape), grads_r[n]
-        if shape[0] != 1:     # conv / linear weights: full-tensor relative L2
-            assert rel(g, gr) < 0.1, (n, rel(g, gr))
-        else:                 # norm gamma / beta [1, C, 1]: norm agreement
-            assert abs(float(g.norm()) / float(gr.norm()) - 1) < 0.1, n
+            e, lim = abs(float(g.reshape(-1)[0] - gr.reshape(-1)[0])) / a_scale, a_lim
+        elif shape[0] == 1:
+            e, lim = rel(g, gr), n_lim
+        else:
+            e, lim = rel(g, gr), w_lim
+        errs[n] = float(e)
+        if e >= lim:
+            bad.append((n, float(e), lim))
+    top = lambda pred: [(n, round(errs[n], 4)) for n in sorted(errs, key=lambda k: -errs[k]) if pred(n)][:5]
+    print("worst weight", top(lambda n: n not in alphas and dict(shapes)[n][0] != 1))
+    print("worst gamma/beta", top(lambda n: n not in alphas and dict(shapes)[n][0] == 1))
+    print("worst alpha (x mean |g_alpha| = %.4g)" % a_scale, top(lambda n: n in alphas))
+    assert not bad, bad
 
 
 @pytest.mark.timeout(900)

@@ -83,3 +83,42 @@ def test_capturable_adam_matches_eager_adam():
                         capturable=True)
     oc.load_state_dict(copy.deepcopy(oa.state_dict()))
     assert [float(s["step"]) for s in oc.state_dict()["state"].values()] == [6.0] * 4
+
+
+def test_capturable_adam_no_step_limit_and_lr_changes():
+    """the capturable Adam reads no table — past the old 2^20-step table it still
+    updates, bit for bit as the eager Adam at the same step count — and an lr change
+    between steps reaches its device lr (both paths compute the bias corrections with the
+    same device code, ctn_optim.hip adam_bias)."""
+    import ctn_optim
+    torch.manual_seed(1)
+    ps = [torch.nn.Parameter(torch.randn(s, device="cuda")) for s in [(300, 7), (5,)]]
+    qs = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    oa = ctn_optim.Adam(ps, lr=1e-3, capturable=True)
+    ob = ctn_optim.Adam(qs, lr=1e-3)
+    for a, b in zip(ps, qs):
+        a.grad = torch.ones_like(a)
+        b.grad = torch.ones_like(b)
+    oa.step()
+    ob.step()
+    big = (1 << 21) + 3
+    for o in (oa, ob):
+        sd = copy.deepcopy(o.state_dict())
+        for st in sd["state"].values():
+            st["step"] = torch.tensor(float(big))
+        o.load_state_dict(sd)
+    for step in range(4):
+        if step == 2:
+            for o in (oa, ob):
+                o.param_groups[0]["lr"] = 3e-4
+        before = [a.detach().clone() for a in ps]
+        for a, b in zip(ps, qs):
+            g = torch.randn_like(a)
+            a.grad, b.grad = g.clone(), g.clone()
+        oa.step()
+        ob.step()
+        for a, b, a0 in zip(ps, qs, before):
+            assert torch.equal(a, b), step
+            assert not torch.equal(a, a0), step          # the update happened
+    assert [float(s["step"]) for s in oa.state_dict()["state"].values()] == [float(big + 4)] * 2
+    assert float(oa.lr_tensor(0)) == pytest.approx(3e-4)

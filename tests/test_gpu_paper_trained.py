@@ -69,3 +69,45 @@ def test_c4_trained_fp32_sisnri_within_0p01db():
     d = np.abs(got - g["sisnri"])
     assert d.max() < 0.01, d.max()
     assert abs(loss - float(g["loss"])) < 1e-3
+
+
+@need_c2
+@pytest.mark.timeout(900)
+def test_paper_trained_bf16_backward_at_bench_dispatch():
+    """Backward with SEPARATING weights at the c2 dispatch: the PIT
+    loss of three utterances {0, 16, 31} of the fixture's 32-utterance batch, run through
+    the whole M=32 bf16 forward/backward (gLN, the 1x1 convs and the depthwise conv act
+    per utterance, so the weight gradients are those three utterances' alone).
+      (1) dispatch: against the same three utterances run alone (M=3) through the same
+          bf16 path, every gradient tensor within 1e-3 relative L2 (only the fixed-order
+          partial sums group differently);
+      (2) values: against the fp32 oracle's gradients of the three utterances, per tensor
+          (the bounds of test_gpu_benchshape.py::_check_grads_bf16)."""
+    import conv_tasnet as ct
+    import pit_criterion as pc
+    from test_gpu_benchshape import _check_grads_bf16, rel
+    c = PF.CFG
+    params, mix, src, g = PF.load()
+    sel = [0, mix.shape[0] // 2, mix.shape[0] - 1]
+
+    def hip_grads(mx, sr, pick):
+        model = ct.ConvTasNet(c.N, c.L, c.B, c.H, c.P, c.X, c.R, c.C).cuda()
+        model.load_state_dict(params)
+        model.act_dtype = torch.bfloat16
+        est = model(mx.cuda())[pick]
+        lens = torch.full((len(sel),), mx.shape[1], dtype=torch.int64, device="cuda")
+        loss = pc.cal_loss(sr.cuda(), est, lens)[0]
+        model.zero_grad()
+        loss.backward()
+        return dict(model.named_parameters()), float(loss)
+
+    p32, l32 = hip_grads(mix, src[sel], sel)
+    p3, l3 = hip_grads(mix[sel], src[sel], list(range(len(sel))))
+    disp = {n: rel(p32[n].grad.detach().cpu(), p3[n].grad.detach().cpu()) for n in p32}
+    worst = sorted(disp.items(), key=lambda kv: -kv[1])[:4]
+    print("M=32 vs M=3 (same bf16 path):", worst, "losses", l32, l3)
+    assert max(disp.values()) < 1e-3, worst
+    _, loss_r, _, grads_r = O.fwd_bwd(c, params, mix[sel], src[sel], torch.full((len(sel),), mix.shape[1]))
+    print("loss bf16", l32, "oracle", loss_r)
+    assert abs(l32 - loss_r) < 0.1
+    _check_grads_bf16(c, p32, grads_r, w_lim=0.1, n_lim=0.25, a_lim=0.3)

@@ -10,6 +10,13 @@
 
 using namespace ctn;
 
+// the library's device error word (ctn_capi.hip), here one word of this process
+uint32_t* ctn::device_error_word() {
+  static uint32_t* w = nullptr;
+  if (!w && hipMalloc(&w, 4) == hipSuccess) (void)hipMemset(w, 0, 4);
+  return w;
+}
+
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 
 static void* dev_fill(size_t bytes, unsigned seed) {
