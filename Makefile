@@ -124,15 +124,35 @@ varlib: build/var/lib$(VAR).so
 
 # round 6: dual GEMM variants by -D flags: build/dv6_<name> from DV6_<name> (tools/gpu.sh mb)
 DV6_base :=
+DV6_p0 := -DCTN_DV_PRIO=0
 DV6_prow := -DCTN_DV_PRIO=1
 DV6_pcol := -DCTN_DV_PRIO=4
 DV6_pmem := -DCTN_DV_PRIO=16
 DV6_pmem2 := -DCTN_DV_PRIO=32
 DV6_partnt0 := -DCTN_PART_NT=0
 DV6_clnc0 := -DCTN_DV_CLNC=0
-DV6_NAMES := base prow pcol pmem pmem2 partnt0 clnc0
+DV6_p17 := -DCTN_DV_PRIO=17
+DV6_p18 := -DCTN_DV_PRIO=18
+DV6_p33 := -DCTN_DV_PRIO=33
+DV6_p48 := -DCTN_DV_PRIO=48
+DV6_p20 := -DCTN_DV_PRIO=20
+DV6_p34 := -DCTN_DV_PRIO=34
+DV6_p49 := -DCTN_DV_PRIO=49
+DV6_p50 := -DCTN_DV_PRIO=50
+DV6_p37 := -DCTN_DV_PRIO=37
+DV6_NAMES := base p0 prow pcol pmem pmem2 partnt0 clnc0 p17 p18 p33 p48 p20 p34 p49 p50 p37
 dv6: $(patsubst %,build/dv6_%,$(DV6_NAMES))
 build/dv6_%: tools/microbench/dual_ws_bench.hip $(PKG)/csrc/ctn_dual_ws.hip $(PKG)/csrc/ctn_gemm_dual.hip $(HDR)
 	@mkdir -p build
 	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -Iinclude $(DEVFLAGS) $(DV6_$*) $< -o $@
 .PHONY: dv6
+
+# round 6: WS GEMM variants by -D flags: build/ws6_<name> from WS6_<name>
+WS6_base :=
+WS6_pp := -DCTN_WS_PP=1
+WS6_NAMES := base pp
+ws6: $(patsubst %,build/ws6_%,$(WS6_NAMES))
+build/ws6_%: tools/microbench/ws_bench.hip $(PKG)/csrc/ctn_gemm_ws.hip $(HDR)
+	@mkdir -p build
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -Iinclude $(DEVFLAGS) $(WS6_$*) $< -o $@
+.PHONY: ws6

@@ -132,13 +132,23 @@ static_assert(DV_CJC == 1 || DV_CJC == 2 || DV_CJC == 4, "column blocks per colu
 #define CTN_DV_C2 0
 #endif
 
-// Static wave priority per role (s_setprio once at the role's start; experiment): bits 0-1
-// row waves, 2-3 column waves, 4-5 memory waves (each a priority 0..3)
+// Static wave priority per role (s_setprio once at the role's start): bits 0-1 row waves,
+// 2-3 column waves, 4-5 memory waves (each a priority 0..3).  The SIMD's issue arbiter
+// serves the higher priority first, so the memory wave sharing a SIMD with three
+// consumers issues each tile's LDS-DMA as soon as its slot is free instead of behind the
+// consumers' MFMA/VALU streams, and the row waves (whose stores feed the next kernel) go
+// before the column waves.  Measured (microbenchmark, bench shape, three alternations on
+// one box): gLN 81-89 us with none, 75-78 us with memory 3 + row 1
+// (CTN_DV_PRIO=49) or memory 2 + row 1 (33); higher column priority slower (89-92 us); the
+// c5 shape 84 -> 76 us; the cLN form (c4) flat to slightly slower, so it keeps none.
 #ifndef CTN_DV_PRIO
-#define CTN_DV_PRIO 0
+#define CTN_DV_PRIO 49
 #endif
-template <int SHIFT> CTN_DEV void dv_prio() {
-  constexpr int pr = (CTN_DV_PRIO >> SHIFT) & 3;
+#ifndef CTN_DV_PRIO_CLN
+#define CTN_DV_PRIO_CLN 0
+#endif
+template <int SHIFT, int NK> CTN_DEV void dv_prio() {
+  constexpr int pr = ((NK == NORM_CLN ? CTN_DV_PRIO_CLN : CTN_DV_PRIO) >> SHIFT) & 3;
   if constexpr (pr != 0) __builtin_amdgcn_s_setprio(pr);
 }
 
@@ -329,7 +339,7 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
   };
   if (wid < NR) {
     // ======================= row waves =======================
-    dv_prio<0>();
+    dv_prio<0, NK>();
     // wave r: output channels n0 + 32r .. +31 of both 16-row blocks of every tile, against
     // the resident W fragments (group 4*sl + r of the fragment-ordered copy, nb = 0, 1):
     // lane (lg, lr) holds channels 32r + 8lg .. +7 (slice-local) of frame rows lr, 16 + lr.
@@ -527,7 +537,7 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
   }
   if (wid < ND) {
     // ======================= column waves =======================
-    dv_prio<2>();
+    dv_prio<2, NK>();
     // wave c = (wp, wn) owns dW2 blocks p in [16 CI wp, +16 CI), n in [n0 + 16 CJ wn, +16 CJ):
     // dW2 += gy_tile^T . op(d)_tile, the reduction over the tile's 32 frame rows
     // the slice's 16 x 8 blocks of 16 x 16: waves in a (NC / (8 / CJ)) x (8 / CJ) grid,
@@ -708,7 +718,7 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
   }
 
   // ======================= memory waves =======================
-  dv_prio<4>();
+  dv_prio<4, NK>();
   // Memory wave m moves, per tile, A blocks 4m..4m+3 (16 rows x 32 channels of gy each),
   // raw-d pieces 2m, 2m+1 (4 rows x the slice's 128 channels each) and its statistics
   // piece by LDS-DMA (buffer_load ... lds: no registers, PF tiles ahead), waits for its

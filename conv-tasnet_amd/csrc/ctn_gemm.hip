@@ -459,6 +459,9 @@ template <typename T> struct ColsCks { static constexpr int v = sizeof(T) == 2 ?
 template <typename T> struct ColsCkr { static constexpr int v = sizeof(T) == 2 ? CTN_COLS_CKR : CKR; };
 constexpr int CKS = 2;                           // k-split groups per workgroup (host-side sizing)
 
+#ifndef CTN_COLS_PRIO
+#define CTN_COLS_PRIO 0
+#endif
 template <typename T, int OPA, int OPB, int NK>
 __global__ __launch_bounds__(256 * ColsCks<T>::v) void gemm_cols_kernel(GemmCols p) {
   constexpr int CKS = ColsCks<T>::v;
@@ -473,6 +476,9 @@ __global__ __launch_bounds__(256 * ColsCks<T>::v) void gemm_cols_kernel(GemmCols
   constexpr int NCH = CKR * CPR / 256;           // chunks per thread per operand
   const int grp = threadIdx.x >> 8;              // k-split group
   char* smem = smem_all + grp * 2 * STAGE;
+  // static priority of one k-split group (experiment): 1 = group 1, 2 = group 0
+  if constexpr (CTN_COLS_PRIO == 1) { if (grp == 1) __builtin_amdgcn_s_setprio(1); }
+  if constexpr (CTN_COLS_PRIO == 2) { if (grp == 0) __builtin_amdgcn_s_setprio(1); }
   const int tid = threadIdx.x & 255, lane = tid & 63, wid = tid >> 6;
   const int wp = wid >> 1, wq = wid & 1;
   const int lr = lane & 15, lg = lane >> 4;

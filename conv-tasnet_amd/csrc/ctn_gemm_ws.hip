@@ -106,6 +106,18 @@ constexpr int WS_FOLD_MAX = 512;   // utterances whose gLN operand stats a workg
 #ifndef CTN_WS_PRIO
 #define CTN_WS_PRIO 0
 #endif
+// Ping-pong (LDS-DMA ring configurations of 16 waves): waves 8-15 run each tile half a
+// tile behind waves 0-7 — two barriers per tile, and between them one half runs its MFMAs
+// while the other runs the previous tile's epilogue and stores, so on every SIMD (two
+// waves of each half) the matrix pipe and the vector/store issue overlap instead of all
+// 16 waves meeting at one barrier and then running the same phase.  Same arithmetic,
+// same results bit for bit.
+#ifndef CTN_WS_PP
+#define CTN_WS_PP 0
+#endif
+#ifndef CTN_WS_HPRIO
+#define CTN_WS_HPRIO 0
+#endif
 #ifndef CTN_WS_STAMP
 #define CTN_WS_STAMP 0
 #endif
@@ -174,6 +186,9 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
+  // static priority for the second half of the waves (experiment; the younger half loses
+  // every issue arbitration otherwise, MI355X_MICROARCH.md "Two waves per SIMD" item 4)
+  if constexpr (CTN_WS_HPRIO != 0) { if (wid >= WV / 2) __builtin_amdgcn_s_setprio(CTN_WS_HPRIO); }
   const int ntile = (int)(p.g.rows() / TM);
   constexpr int NS = WV * 16 * NB;             // output channels per slice
   const int nr = (int)gridDim.x / S;           // row ranges
@@ -715,6 +730,45 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
           }
           epilogue_math(le1, t, acc);
           store_out(t);
+        }
+      } else if constexpr (CTN_WS_PP && WV == 16) {
+        // ping-pong: half 0 (waves 0-7) MFMA(t) | epilogue(t); half 1 (waves 8-15)
+        // epilogue(t-1) | MFMA(t), the two phases of tile t separated by a barrier.  The
+        // slot refilled at iteration t (tile t-1's) was last read by half 1 in phase 2
+        // of iteration t-1, before this iteration's first barrier.
+        const bool late = wid >= WV / 2;
+        for (int t = t0; t < t1; ++t) {
+          {
+            // half 1 has stored nothing in iteration t0 (no tile t0 - 1): one store group
+            // fewer behind the DMA of tile t, so its count is one group stricter
+            constexpr int NST = NFW * (WS_DR - 2) + SPT * (WS_DR - 1);   // steady state
+            const int ds = t - t0 - (late ? 1 : 0);
+            const int n = NFW * mn(WS_DR - 2, t1 - 1 - t) + SPT * mn(WS_DR - 1, ds < 0 ? 0 : ds);
+            if (n == NST) vmwait_c<NST>();
+            else vmwait23(n);
+          }
+          lds_barrier();
+          dma(t + WS_DR - 1);
+          if (!late) {
+            mfma_tile(sA[t % WS_DR], acc);
+          } else if (t > t0) {
+            epilogue_math(le1, t - 1, acc);
+            store_out(t - 1);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          lds_barrier();
+          if (t > t0) cln_final(t - 1);   // both halves' partials of tile t - 1 are in LDS
+          if (!late) {
+            epilogue_math(le1, t, acc);
+            store_out(t);
+          } else {
+            mfma_tile(sA[t % WS_DR], acc);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if (late) {
+          epilogue_math(le1, t1 - 1, acc);
+          store_out(t1 - 1);
         }
       } else
       for (int t = t0; t < t1; ++t) {
