@@ -125,6 +125,32 @@ def copy_peak_gbs(dev, lib, sizes_mib=(256, 512, 1024), reps=10):
     return res[name], name
 
 
+def mfma_peak_tflops(dev, lib, reps=5):
+    """Measured matrix peak of this GPU (a measured MFMA microbenchmark
+    beside the 2.5 PF/s datasheet value): ctn_mfma_peak, back-to-back bf16 MFMAs on random
+    register operands, 2 workgroups of 4 waves per CU, best of `reps` launches per shape.
+    Returns {shape: TFLOP/s}."""
+    import ctn_lib as L
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    wgs = 2 * torch.cuda.get_device_properties(dev).multi_processor_count
+    out = torch.empty(wgs * 256, dtype=torch.float32, device=dev)
+    res = {}
+    for shape, name, iters in ((0, "v_mfma_f32_16x16x32_bf16", 8000), (1, "v_mfma_f32_32x32x16_bf16", 8000)):
+        flops = ctypes.c_double(0.0)
+        best = float("inf")
+        for _ in range(reps + 1):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            L.check(lib.ctn_mfma_peak(shape, wgs, iters, out.data_ptr(), ctypes.byref(flops), stream), "ctn_mfma_peak")
+            e1.record()
+            e1.synchronize()
+            best = min(best, e0.elapsed_time(e1))
+        res[name] = round(flops.value / (best * 1e-3) / 1e12, 1)
+    if not torch.isfinite(out).all():
+        raise RuntimeError("bench.py: the MFMA microbenchmark produced non-finite values")
+    return res
+
+
 def dual_pair_a():
     """Pair A of the dual GEMM (ctn_gemm_dual.hip) is on unless CTN_GEMM_DUAL clears bit 0."""
     return bool(int(os.environ.get("CTN_GEMM_DUAL", "1")) & 1)
@@ -311,8 +337,8 @@ def main():
     ap.add_argument("--fp32", action="store_true", help="fp32 activations (parity mode) instead of bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-copy-peak", action="store_true",
-                    help="skip the streaming-ceiling calibration (copy_peak: null); profiling runs use it so "
-                         "that no calibration copy lands in a kernel trace")
+                    help="skip the calibration kernels after the timed steps (copy_peak and mfma_peak: null); "
+                         "profiling runs use it so that no calibration kernel lands in a kernel trace")
     ap.add_argument("--timer-kind", type=int, default=0,
                     help="kernel timed in the timed region (default: the dominant one of the profile pass)")
     ap.add_argument("--timer-stride", type=int, default=9,
@@ -491,6 +517,7 @@ def main():
     final_loss = float(loss.detach())
     deferred = (ctn_ops.DEFERRED_BLOCKS - n_def0) / args.steps
     copy_gbs, copy_how = copy_peak_gbs(dev, lib) if rank == 0 and not args.no_copy_peak else (None, None)
+    mfma_peak = mfma_peak_tflops(dev, lib) if rank == 0 and not args.no_copy_peak else None
 
     if rank == 0:
         s = s_el
@@ -559,6 +586,8 @@ def main():
                          # rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * 1024 SIMDs) of
                          # this kernel, from the committed PMC pass (profiles/pmc_mfma.json)
                          "mfma_util": mfma.get("mfma_util") if mfma else None,
+                         # measured matrix peak (ctn_mfma_peak) beside the dense bf16 datasheet value
+                         "mfma_peak": {"measured_tflops": mfma_peak, "datasheet_tflops": BF16_PEAK_TFLOPS},
                          # the whole step against the same peak: SURVEY §8d compulsory bytes
                          "step_frac": round(step_alg_bytes(M, K, T, cfg, s) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                          # every TemporalBlock kernel family, timed live in the untimed profile

@@ -104,6 +104,14 @@ extern "C" int ctn_copy_bytes(void* dst, const void* src, size_t bytes, int work
   return CTN_OK;
 }
 
+extern "C" int ctn_mfma_peak(int shape, int workgroups, int iters, float* out, double* flops, void* stream) {
+  if (!out || workgroups < 1 || workgroups > 65536 || iters < 1 || (shape != 0 && shape != 1))
+    return fail(CTN_ERR_ARG, "mfma_peak: shape %d, %d workgroups, %d iterations (shape 0|1, 1..65536, >= 1)", shape,
+                workgroups, iters);
+  CTN_HIP(ctn::launch_mfma_peak(shape, workgroups, iters, out, flops, (hipStream_t)stream));
+  return CTN_OK;
+}
+
 extern "C" int ctn_timer_enable(int kind, int max_launches) {
   if (kind < 0 || kind >= 32) return fail(CTN_ERR_ARG, "timer kind %d", kind);
   return ctn_timer_enable_mask(kind ? 1u << kind : 0u, kind ? max_launches : 0);

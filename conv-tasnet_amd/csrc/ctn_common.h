@@ -80,8 +80,8 @@ CTN_DEV void stg16(void* p, v4u v) {
 #ifndef CTN_PART_NT
 #define CTN_PART_NT 1
 #endif
-CTN_DEV void st_part(float* p, float v) {
-  if constexpr (CTN_PART_NT != 0) __builtin_nontemporal_store(v, p);
+template <bool NT = (CTN_PART_NT != 0)> CTN_DEV void st_part(float* p, float v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
   else *p = v;
 }
 // the same with the nontemporal hint when NT (per-kernel choice)

@@ -711,7 +711,13 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
         } else {
           const int n = n0 + (wn * CJ + j) * 16 + lr;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) st_part(&Dp[(size_t)((wp * CI + i) * 16 + 4 * lg + e) * p.Nout + n], dacc[i][j][e]);
+          // nontemporal for gLN (c2, c5: keeps the activations of the next kernels in the
+          // Infinity Cache); plain for cLN: at c4 every tensor is larger than the cache and
+          // the hinted dword stores measured 10 us slower per launch (547.7 / 533.6 against
+          // 555.3 / 544.7 us, microbenchmark, round 6) — the c4 regression of round 5
+          for (int e = 0; e < 4; ++e)
+            st_part<CTN_PART_NT != 0 && NK == NORM_GLN>(&Dp[(size_t)((wp * CI + i) * 16 + 4 * lg + e) * p.Nout + n],
+                                                        dacc[i][j][e]);
         }
       }
     return;

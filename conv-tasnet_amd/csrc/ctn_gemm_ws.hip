@@ -152,8 +152,10 @@ CTN_DEV void ready(float v) { asm volatile("" ::"v"(v)); }
 // S: output-channel slices; workgroup b -> (row range rr, slice sl), the S slices of
 // a range on one XCD (hardware ids are dealt round-robin over the 8 XCDs) so the A
 // tile comes from HBM once.  Each slice-workgroup holds NS = WV*16*NB channels.
+// (S = 2: two 8-wave slice workgroups share a CU, CTN_WS_S512; S = 3: the three 512-channel
+// slices of a 1536-channel output (c5's mask conv, C*N = 3*512) on three CUs of one XCD.)
 template <int OPK, int NK, int EPI, int NB, int KB, int WV, int MB, int S = 1>
-__global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p) {
+__global__ __launch_bounds__(64 * WV, (S == 2 ? 2 : 1) * WV / 4) void gemm_ws_kernel(GemmRows p) {
   constexpr int NT = 64 * WV;                  // threads
   constexpr int TM = 16 * MB;                  // frame rows per tile
   constexpr int KR = KB * 32;                  // reduction length
@@ -896,6 +898,16 @@ __global__ __launch_bounds__(64 * WV, S * WV / 4) void gemm_ws_kernel(GemmRows p
 // ---------------------------------------------------------------------------
 // dispatch
 // ---------------------------------------------------------------------------
+// CTN_WS_1536=0: c5's 1536-channel mask conv on the tiled gemm_rows kernel instead (A/B)
+static bool ws1536_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("CTN_WS_1536");
+    on = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  return on == 1;
+}
+
 static bool ws_enabled() {
   static int on = -1;
   if (on < 0) {
@@ -907,7 +919,7 @@ static bool ws_enabled() {
 
 // (Nout, Kred) shapes with a resident-weight instantiation
 static bool ws_shape(int Nout, int Kred, int* nb, int* kb) {
-  if (Nout == 512 && Kred == 256) { *nb = 4; *kb = 8; return true; }
+  if ((Nout == 512 || Nout == 1536) && Kred == 256) { *nb = 4; *kb = 8; return true; }
   if (Nout == 256 && Kred == 512) { *nb = 2; *kb = 16; return true; }
   if (Nout == 256 && Kred == 256) { *nb = 2; *kb = 8; return true; }
   return false;
@@ -922,6 +934,8 @@ static bool ws_pair(int opk, int epi) {   // (operand op, epilogue) pairs used o
 bool gemm_ws_eligible(DType dt, const GemmRows& p) {
   int nb, kb;
   if (dt != BF16 || !ws_enabled() || !ws_shape(p.Nout, p.Kred, &nb, &kb) || !ws_pair(p.aop.kind, p.epi)) return false;
+  // 1536 outputs (c5's mask conv): the plain-operand store form only, as three slices
+  if (p.Nout == 1536 && (p.aop.kind != OP_PLAIN || p.epi != EPI_STORE || !ws1536_enabled())) return false;
   if (p.g.Kp % WS_TM || p.lda % 8 || p.ldw % 8 || p.ldc % 8) return false;
   // 32-bit tile offsets and buffer sizes (the LDS-DMA ring's du_rsrc clamps at 2^31 bytes)
   if (p.g.rows() * (p.Kred > p.Nout ? p.Kred : p.Nout) * 2 >= (1L << 31)) return false;
@@ -954,7 +968,10 @@ static int ws_slices(const GemmRows& p);
 
 static int ws_ranges(const GemmRows& p) {
   const long nt = p.g.rows() / ws_tile_rows(p);
-  return (int)(nt < WS_GRID ? nt : WS_GRID);
+  // three 16-wave slice workgroups per range fill the CUs once: 80 ranges (a multiple of
+  // 8, so a range's slices share an XCD and its L2 copy of the A tile)
+  const int cap = ws_slices(p) == 3 ? (WS_GRID / 3) / 8 * 8 : WS_GRID;
+  return (int)(nt < cap ? nt : cap);
 }
 int gemm_ws_grid(const GemmRows& p) { return ws_ranges(p) * ws_slices(p); }
 
@@ -978,12 +995,12 @@ int gemm_ws_group_parts(const GemmRows& p) {
   return (int)((entries + p.g.M - 1) / p.g.M);
 }
 
-static bool ws_wide(const GemmRows& p) {   // Nout = 512 on 32-row tiles (16 waves per range)
-  return p.Nout == 512 && p.Kred == 256 && p.epi != EPI_NORM_BWD;
+static bool ws_wide(const GemmRows& p) {   // Nout = 512 (or 3 x 512) on 32-row tiles (16 waves per range)
+  return (p.Nout == 512 || p.Nout == 1536) && p.Kred == 256 && p.epi != EPI_NORM_BWD;
 }
-static int ws_waves(const GemmRows& p) { return ws_wide(p) ? 16 : 8; }
+static int ws_waves(const GemmRows& p) { return ws_wide(p) ? 16 * (p.Nout / 512) : 8; }
 static int ws_tile_rows(const GemmRows& p) { return ws_wide(p) ? 32 : WS_TM; }
-static int ws_slices(const GemmRows& p) { return ws_wide(p) ? CTN_WS_S512 : 1; }
+static int ws_slices(const GemmRows& p) { return p.Nout == 1536 ? 3 : ws_wide(p) ? CTN_WS_S512 : 1; }
 
 // Register-staged kernel configurations: (NB, KB, waves, m-blocks, slices).  Nout = 512
 // runs 16 waves of 32 channels per 32-row range (64 weight VGPRs per lane: 4 waves
@@ -998,7 +1015,10 @@ static hipError_t ws_launch_shape(const GemmRows& p, hipStream_t s) {
   if (nb == 4 && kb == 8) {
     if constexpr (EPI == EPI_NORM_BWD)   // its epilogue needs more than the 128 registers of 16 waves
       hipLaunchKernelGGL((gemm_ws_kernel<OPK, NK, EPI, 4, 8, 8, 1>), grid, dim3(512), 0, s, p);
-    else if (ws_slices(p) == 2)
+    else if (ws_slices(p) == 3) {
+      if constexpr (OPK == OP_PLAIN && EPI == EPI_STORE)
+        hipLaunchKernelGGL((gemm_ws_kernel<OPK, NK, EPI, 2, 8, 16, 2, 3>), grid, dim3(1024), 0, s, p);
+    } else if (ws_slices(p) == 2)
       hipLaunchKernelGGL((gemm_ws_kernel<OPK, NK, EPI, 2, 8, 8, 2, 2>), grid, dim3(512), 0, s, p);
     else
       hipLaunchKernelGGL((gemm_ws_kernel<OPK, NK, EPI, 2, 8, 16, 2>), grid, dim3(1024), 0, s, p);

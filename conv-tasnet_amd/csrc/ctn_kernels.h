@@ -161,6 +161,8 @@ void slab_reduce_assign_tmp(const SlabDesc* d, int n, float* tmp, float** out);
 // any number of descriptors, tmps[i] = descriptor i's scratch (null: one pass)
 hipError_t launch_slab_reduce_list(const SlabDesc* d, float* const* tmps, int n, hipStream_t s);
 hipError_t launch_copy_stream(void* dst, const void* src, size_t bytes, int wgs, int flags, hipStream_t s);   // 16-B aligned
+// MFMA throughput microbenchmark (ctn_mfma_peak): *flops = the FLOP the launch performs
+hipError_t launch_mfma_peak(int shape, int wgs, int iters, float* out, double* flops, hipStream_t s);
 
 // fp32 weight [O][I] -> storage-type copy (Ws, [O][I]) and/or transpose (Wt, [I][O])
 hipError_t launch_prep_weight(DType dt, const float* W, int O, int I, void* Ws, void* Wt,

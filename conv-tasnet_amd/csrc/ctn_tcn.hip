@@ -844,6 +844,59 @@ hipError_t launch_copy_stream(void* dst, const void* src, size_t bytes, int wgs,
   return hipGetLastError();
 }
 
+// MFMA throughput microbenchmark (bench.py's measured matrix peak beside the 2.5 PF/s
+// datasheet value, ctn_mfma_peak): every wave issues `iters` rounds of NACC independent
+// back-to-back bf16 MFMAs on register operands drawn from a hash of its lane (random
+// data: the chip holds a lower clock on random than on zero operands), and writes its
+// accumulators so nothing is dead.  SHAPE 0: v_mfma_f32_16x16x32_bf16 (16384 FLOP, the
+// block kernels' instruction), 1: v_mfma_f32_32x32x16_bf16 (32768 FLOP).
+typedef short mp_bf16x8 __attribute__((ext_vector_type(8)));
+typedef float mp_f32x4 __attribute__((ext_vector_type(4)));
+typedef float mp_f32x16 __attribute__((ext_vector_type(16)));
+template <int SHAPE>
+__global__ __launch_bounds__(256) void mfma_peak_kernel(int iters, float* out) {
+  constexpr int NACC = SHAPE == 0 ? 8 : 4;
+  const uint32_t gid = blockIdx.x * 256u + threadIdx.x;
+  uint32_t h = gid * 2654435761u + 12345u;
+  short av[8], bv[8];
+  for (int e = 0; e < 8; ++e) {
+    h ^= h << 13; h ^= h >> 17; h ^= h << 5;
+    av[e] = (short)(0x3800 | (h & 0x807f));   // bf16 of magnitude ~2^-15..2^-14, random sign and mantissa
+    h ^= h << 13; h ^= h >> 17; h ^= h << 5;
+    bv[e] = (short)(0x3800 | (h & 0x807f));
+  }
+  const mp_bf16x8 a = {av[0], av[1], av[2], av[3], av[4], av[5], av[6], av[7]};
+  const mp_bf16x8 b = {bv[0], bv[1], bv[2], bv[3], bv[4], bv[5], bv[6], bv[7]};
+  float sum = 0.f;
+  if constexpr (SHAPE == 0) {
+    mp_f32x4 acc[NACC];
+    for (int j = 0; j < NACC; ++j) acc[j] = mp_f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int it = 0; it < iters; ++it)
+#pragma unroll
+      for (int j = 0; j < NACC; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[j], 0, 0, 0);
+    for (int j = 0; j < NACC; ++j) sum += acc[j][0] + acc[j][1] + acc[j][2] + acc[j][3];
+  } else {
+    mp_f32x16 acc[NACC];
+    for (int j = 0; j < NACC; ++j)
+      for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+    for (int it = 0; it < iters; ++it)
+#pragma unroll
+      for (int j = 0; j < NACC; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[j], 0, 0, 0);
+    for (int j = 0; j < NACC; ++j)
+      for (int e = 0; e < 16; ++e) sum += acc[j][e];
+  }
+  out[gid] = sum;
+}
+
+hipError_t launch_mfma_peak(int shape, int wgs, int iters, float* out, double* flops, hipStream_t s) {
+  if (!out || wgs < 1 || wgs > 65536 || iters < 1 || (shape != 0 && shape != 1)) return hipErrorInvalidValue;
+  // waves x iterations x independent accumulators x FLOP per instruction
+  if (flops) *flops = (double)wgs * 4 * iters * (shape == 0 ? 8.0 * 16384 : 4.0 * 32768);
+  if (shape == 0) hipLaunchKernelGGL((mfma_peak_kernel<0>), dim3(wgs), dim3(256), 0, s, iters, out);
+  else hipLaunchKernelGGL((mfma_peak_kernel<1>), dim3(wgs), dim3(256), 0, s, iters, out);
+  return hipGetLastError();
+}
+
 __global__ __launch_bounds__(256) void slab_reduce_kernel(SrBatch b) {
   __shared__ double part[4][64];
   __shared__ double part4[4][4][64];

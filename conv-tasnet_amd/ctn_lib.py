@@ -174,6 +174,8 @@ _SIGS = {
     "ctn_timer_set_stride": (ctypes.c_int, [ctypes.c_int]),
     "ctn_copy_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
                                       ctypes.c_void_p]),
+    "ctn_mfma_peak": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_void_p]),
     "ctn_timer_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
     "ctn_timer_enable_mask": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_int]),
     "ctn_timer_read_kind": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_double),

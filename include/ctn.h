@@ -438,6 +438,12 @@ int ctn_timer_set_stride(int stride);
 #define CTN_COPY_NT 1
 #define CTN_COPY_DEEP 2
 int ctn_copy_bytes(void* dst, const void* src, size_t bytes, int workgroups, int flags, void* stream);
+/* ABI v12: an MFMA throughput microbenchmark (bench.py's measured matrix peak beside the
+ * 2.5 PF/s datasheet value): `workgroups` x 4 waves, each issuing `iters` rounds of
+ * independent back-to-back bf16 MFMAs on random register operands — shape 0
+ * v_mfma_f32_16x16x32_bf16 (8 accumulators), 1 v_mfma_f32_32x32x16_bf16 (4) — writing
+ * workgroups*256 floats to `out`; *flops (may be NULL) = the FLOP of the launch. */
+int ctn_mfma_peak(int shape, int workgroups, int iters, float* out, double* flops, void* stream);
 
 /* -------------------------------------------------------------------------
  * Device error word (ABI v9).  Kernels whose waves hand tiles to each other through

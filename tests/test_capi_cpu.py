@@ -199,3 +199,14 @@ def test_pit_speaker_range(lib):
     for C, ok in ((1, True), (8, True), (9, True), (16, True), (17, False)):
         n = lib.ctn_pit_workspace_bytes(ctypes.byref(L.PitDesc(4, C, 1000)))
         assert (n > 0) == ok, (C, n)
+
+
+def test_mfma_peak_validation(lib):
+    """ctn_mfma_peak (bench calibration microbenchmark) checks its arguments before launching."""
+    buf = ctypes.create_string_buffer(64)
+    p = ctypes.addressof(buf)
+    assert lib.ctn_mfma_peak(0, 1, 1, None, None, None) == 1          # no output
+    assert lib.ctn_mfma_peak(2, 1, 1, p, None, None) == 1             # unknown shape
+    assert "shape" in lib.ctn_last_error().decode()
+    assert lib.ctn_mfma_peak(0, 0, 1, p, None, None) == 1             # no workgroups
+    assert lib.ctn_mfma_peak(1, 1, 0, p, None, None) == 1             # no iterations

@@ -17,3 +17,29 @@ def test_copy_bytes(n16, wgs, flags):
     L.check(lib.ctn_copy_bytes(b.data_ptr(), a.data_ptr(), n16 * 16, wgs, flags, s), "ctn_copy_bytes")
     torch.cuda.synchronize()
     assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [0, 1])
+def test_mfma_peak(shape):
+    """ctn_mfma_peak, bench.py's matrix-peak calibration: the reported FLOP count and a
+    finite output, at a rate between a tenth of and the 2.5 PF/s dense datasheet peak."""
+    import ctypes
+    import ctn_lib as L
+    lib = L.load()
+    dev = torch.device("cuda")
+    wgs, iters = 512, 4000
+    out = torch.full((wgs * 256,), float("nan"), device=dev)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    flops = ctypes.c_double(0.0)
+    L.check(lib.ctn_mfma_peak(shape, wgs, iters, out.data_ptr(), ctypes.byref(flops), s), "ctn_mfma_peak")
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    L.check(lib.ctn_mfma_peak(shape, wgs, iters, out.data_ptr(), None, s), "ctn_mfma_peak")
+    e1.record()
+    e1.synchronize()
+    assert flops.value == wgs * 4 * iters * (8 * 16384 if shape == 0 else 4 * 32768)
+    assert torch.isfinite(out).all()
+    tflops = flops.value / (e0.elapsed_time(e1) * 1e-3) / 1e12
+    print("shape", shape, "TFLOP/s", tflops)
+    assert 250 < tflops < 2600
