@@ -140,7 +140,30 @@ DV6_p34 := -DCTN_DV_PRIO=34
 DV6_p49 := -DCTN_DV_PRIO=49
 DV6_p50 := -DCTN_DV_PRIO=50
 DV6_p37 := -DCTN_DV_PRIO=37
-DV6_NAMES := base p0 prow pcol pmem pmem2 partnt0 clnc0 p17 p18 p33 p48 p20 p34 p49 p50 p37
+DV6_la2 := -DCTN_DV_LA=2
+DV6_pf4 := -DCTN_DV_PF=4
+DV6_pf3 := -DCTN_DV_PF=3
+DV6_nc4 := -DCTN_DV_NC=4 -DCTN_DV_CJ=2
+DV6_la0 := -DCTN_DV_LA=0
+DV6_e1 := -DCTN_DV_EXP=1
+DV6_e2 := -DCTN_DV_EXP=2
+DV6_e64 := -DCTN_DV_EXP=64
+DV6_e32 := -DCTN_DV_EXP=32
+DV6_e34 := -DCTN_DV_EXP=34
+DV6_e96 := -DCTN_DV_EXP=96
+DV6_e4 := -DCTN_DV_EXP=4
+DV6_e8 := -DCTN_DV_EXP=8
+DV6_st := -DCTN_DV_STAMP=1
+DV6_st2 := -DCTN_DV_STAMP=1 -DCTN_DV_EXP=2
+DV6_st64 := -DCTN_DV_STAMP=1 -DCTN_DV_EXP=64
+DV6_st0 := -DCTN_DV_STAMP=1 -DCTN_DV_PRIO=0
+DV6_r8p0 := -DCTN_DV8_PRIO=0
+DV6_r8p4 := -DCTN_DV8_PRIO=4
+DV6_r8p9 := -DCTN_DV8_PRIO=9
+DV6_r8p8 := -DCTN_DV8_PRIO=8
+DV6_r8la1 := -DCTN_DV8_LA=1
+DV6_r8la3 := -DCTN_DV8_LA=3
+DV6_NAMES := r8p0 r8p4 r8p9 r8p8 r8la1 r8la3 st st2 st64 st0 e1 e2 e64 e32 e34 e96 e4 e8 la2 pf4 pf3 nc4 la0 base p0 prow pcol pmem pmem2 partnt0 clnc0 p17 p18 p33 p48 p20 p34 p49 p50 p37
 dv6: $(patsubst %,build/dv6_%,$(DV6_NAMES))
 build/dv6_%: tools/microbench/dual_ws_bench.hip $(PKG)/csrc/ctn_dual_ws.hip $(PKG)/csrc/ctn_gemm_dual.hip $(HDR)
 	@mkdir -p build

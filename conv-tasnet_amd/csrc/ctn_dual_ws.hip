@@ -152,6 +152,15 @@ template <int SHIFT, int NK> CTN_DEV void dv_prio() {
   if constexpr (pr != 0) __builtin_amdgcn_s_setprio(pr);
 }
 
+// gemm_dual_r8_kernel (gLN): static priorities (bits 0-1 row waves, 2-3 column waves) and
+// the row waves' A-fragment look-ahead
+#ifndef CTN_DV8_PRIO
+#define CTN_DV8_PRIO 1
+#endif
+#ifndef CTN_DV8_LA
+#define CTN_DV8_LA 2
+#endif
+
 // Row waves: A fragments read LA k-steps ahead of their MFMAs
 #ifndef CTN_DV_LA
 #define CTN_DV_LA 1
@@ -175,6 +184,37 @@ constexpr int DV_LA = CTN_DV_LA;
 // bit 3 is the bench's own (per-launch statistics dump).
 #ifndef CTN_DV_DBG
 #define CTN_DV_DBG 0
+#endif
+
+// Diagnostic build only (tools/microbench/dual_ws_bench.hip -DCTN_DV_STAMP=1): per wave,
+// s_memtime cycles spent in each wait (row/column: FULL polls; memory: own-DMA vmcnt
+// waits and DONE polls) and in the whole tile loop, summed into dv_stamps[wg][wave][4]
+#ifndef CTN_DV_STAMP
+#define CTN_DV_STAMP 0
+#endif
+#if CTN_DV_STAMP
+__device__ unsigned long long dv_stamps[1024 * 16 * 4];
+#define DV_TS(v) unsigned long long v = __builtin_amdgcn_s_memtime()
+#define DV_ACC(i, t0v) st_acc[i] += __builtin_amdgcn_s_memtime() - (t0v)
+#define DV_STAMP_DECL unsigned long long st_acc[4] = {0, 0, 0, 0}
+#define DV_STAMP_STORE                                                                    \
+  do {                                                                                    \
+    if (lane == 0)                                                                        \
+      for (int i_ = 0; i_ < 4; ++i_) dv_stamps[((size_t)blockIdx.x * 16 + wid) * 4 + i_] = st_acc[i_]; \
+  } while (0)
+#else
+#define DV_TS(v) \
+  do {           \
+  } while (0)
+#define DV_ACC(i, t0v) \
+  do {                 \
+  } while (0)
+#define DV_STAMP_DECL \
+  do {                \
+  } while (0)
+#define DV_STAMP_STORE \
+  do {                 \
+  } while (0)
 #endif
 
 // slot layout (bytes)
@@ -369,6 +409,7 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
     const int ro = DV_RB ? OFF_B + dv_rbgr(lr, 4 * r + lg)          // row lr; row 16 + lr at + 4096
                          : OFF_R + dv_roff(lr, 4 * r + lg);
 
+    DV_STAMP_DECL;
     double run_s = 0.0, run_q = 0.0;
     const int m0 = t0 / tpu;
     int run_m = m0;
@@ -381,8 +422,11 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
       constexpr bool LE1 = decltype(le1)::value;
       int slot = 0;
       uint32_t gen = 1;
+      DV_TS(tl0);
       for (int t = t0; t < t1; ++t) {
+        DV_TS(tw0);
         dv_wait<4>(fl_full[slot], gen, p.err);
+        DV_ACC(0, tw0);
         char* base = smem + slot * SLOT;
         if constexpr (CTN_DV_EXP & 16) {   // C stores only (zeros)
 #pragma unroll
@@ -527,12 +571,14 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
           ++gen;
         }
       }
+      DV_ACC(3, tl0);
     };
     if (t0 < t1) {
       if (eal <= 1.f) run(std::true_type{});
       else run(std::false_type{});
       if constexpr (NK == NORM_GLN) flush();
     }
+    DV_STAMP_STORE;
     return;
   }
   if (wid < ND) {
@@ -545,6 +591,7 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
     constexpr int CJ = COLS ? DV_CJC : (DV_NI ? CTN_DV_CJN : DV_CJ), CI = 16 * (8 / CJ) / DV_NC;
     static_assert(CI >= 2 && CI <= 16 && CI % 2 == 0, "column split");
     const int c = wid - NR, wp = c / (8 / CJ), wn = c % (8 / CJ);
+    DV_STAMP_DECL;
     f32x4_t dacc[CI][CJ];
 #pragma unroll
     for (int i = 0; i < CI; ++i)
@@ -658,8 +705,11 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
           dv_signal(&fl_done[s1][NR + c], g1);
         }
       }
+      DV_TS(tl0);
       for (; t < t1; ++t) {
+        DV_TS(tw0);
         dv_wait<4>(full_word(slot), gen, p.err);
+        DV_ACC(0, tw0);
         const char* base = smem + slot * SLOT;
         if constexpr (!(CTN_DV_EXP & 3)) {
           bf16x8_t bfr[CJ];
@@ -677,9 +727,11 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
           ++gen;
         }
       }
+      DV_ACC(3, tl0);
     };
     if (COLS || bal <= 1.f) run(std::true_type{});
     else run(std::false_type{});
+    DV_STAMP_STORE;
     // dW2 partial of this workgroup: lane holds D[(wp*CI+i)*16 + 4lg + e][n0 + (wn*CJ+j)*16 + lr]
     float* Dp = p.Dpart + (size_t)rr * KR * p.Nout;
     if constexpr (COLS) {
@@ -734,6 +786,7 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
   // the tile that used it last.  RAWB=1: the raw-d pieces land in the B image itself and
   // wave 0 alone fetches the tile's statistics (all 32 rows).
   const int mw = wid - ND;
+  DV_STAMP_DECL;
   const rsrc_t rA = du_rsrc(p.A, rows * p.lda * 2), rD = du_rsrc(p.Bm, rows * p.ldb * 2);
   const rsrc_t rS = du_rsrc(p.bop.stats, (NK == NORM_GLN ? (long)p.g.M : rows) * 8);
   int arow[4];
@@ -816,23 +869,28 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
       if (t0 + i < t1) dma(t0 + i);
     int slot = 0;
     uint32_t gen = 1;
+    DV_TS(tl0);
     for (int t = t0; t < t1; ++t) {
       const int later = t1 - 1 - t < PF - 1 ? t1 - 1 - t : PF - 1;   // DMA groups issued after tile t's
       char* base = smem + slot * SLOT;
       // tile t's DMA group done: every group issued after it may stay in flight (steady
       // state: PF - 1 of them, a compile-time count; the tail waits for all)
+      DV_TS(tv0);
       if (later == PF - 1) {
         if (!DV_RB || st_wave) dv_vmwait_c<7 * (PF - 1)>();
         else dv_vmwait_c<6 * (PF - 1)>();
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
+      DV_ACC(1, tv0);
       if constexpr (!DV_RB) transform(le1, t, base);
       dv_signal(&fl_full[slot][mw], gen);
       const int tn = t + PF;
       if (tn < t1) {
         const int kn = tn - t0;   // its slot was last used by tile tn - NSL: wait for every DONE of it
+        DV_TS(td0);
         dv_wait<ND>(fl_done[kn % NSL], (uint32_t)(kn / NSL), p.err);
+        DV_ACC(2, td0);
         dma(tn);
       }
       if (++slot == NSL) {
@@ -840,17 +898,287 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
         ++gen;
       }
     }
+    DV_ACC(3, tl0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA may land after the wave ends
   };
   if (t0 < t1) {
     if (COLS || bal <= 1.f) run(std::true_type{});
     else run(std::false_type{});
   }
+  DV_STAMP_STORE;
   if constexpr (COLS) {   // the column waves' two barriers, then a share of the stores
     __syncthreads();
     __syncthreads();
     store_tr(p.Dpart + (size_t)rr * KR * p.Nout);
   }
+}
+
+// ---------------------------------------------------------------------------
+// gLN form with eight row waves (CTN_DUAL_R8, round 6).  Wait stamps of the kernel above
+// (CTN_DV_STAMP) put its critical path in the row waves: busy 84 % of
+// their loop against 64 % for the column waves, while the memory waves idle 55 % waiting
+// for the consumers.  Here the row GEMM of a tile is split by row block over two waves per
+// SIMD (wave (r, rb): output channels n0 + 32r .. +31, frame rows 16rb .. 16rb + 15; same
+// resident W2 fragments, same MFMA sequence per output, so C is bit-identical), and the
+// memory role moves into the column waves, which had the slack: column wave c LDS-DMAs
+// A pieces 2c, 2c + 1, raw-d piece c and (c = 0) the tile's statistics, publishes FULL for
+// its share once its own vmcnt says the share landed, and refills the slot of tile t - 1
+// with tile t + PF after every consumer's DONE of it.  16 waves: 8 row, 8 column.  The
+// norm-2 statistics partials are per (range, slice, row wave): 8 waves per slice
+// (dual_ws_row_waves).
+template <int NSL, int PF>
+__global__ __launch_bounds__(1024) void gemm_dual_r8_kernel(GemmDual p) {
+  constexpr int TM = DV_TM, KB = DV_KB, KR = DV_KR, NS = DV_NS, SLOT = DV_SLOT;
+  constexpr int NRW = 8, NCW = 8;
+  static_assert(DV_RB, "raw-B slot layout");
+  static_assert(NSL * SLOT <= 160 * 1024 - 2048, "LDS budget");
+  __shared__ __attribute__((aligned(16))) char smem[NSL * SLOT];
+  __shared__ __attribute__((aligned(16))) uint32_t fl_full[NSL][NCW];          // per column wave (its DMA share)
+  __shared__ __attribute__((aligned(16))) uint32_t fl_done[NSL][NRW + NCW];    // per consumer
+  __shared__ __attribute__((aligned(16))) float sgb[2][NS];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane & 15, lg = lane >> 4;
+  const int S = p.Nout / NS;
+  const int nr = (int)gridDim.x / S;
+  int rr, sl;
+  {
+    const int b = (int)blockIdx.x;
+    if ((int)gridDim.x % (8 * S) == 0) {
+      const int l = b / 8;
+      sl = l % S;
+      rr = (b % 8) * (nr / 8) + l / S;
+    } else {
+      sl = b % S;
+      rr = b / S;
+    }
+  }
+  const long rows = p.g.rows();
+  const int ntile = (int)(rows / TM);
+  const int t0 = (int)((long)ntile * rr / nr), t1 = (int)((long)ntile * (rr + 1) / nr);
+  const int n0 = sl * NS;
+  const int Kp = p.g.Kp, Kv = p.g.K, tpu = Kp / TM;
+
+  if (tid < NSL * NCW) (&fl_full[0][0])[tid] = 0u;
+  else if (tid < NSL * (NCW + NRW + NCW)) (&fl_done[0][0])[tid - NSL * NCW] = 0u;
+  if (tid < 2 * NS) sgb[tid / NS][tid % NS] = (tid < NS ? p.bop.gamma : p.bop.beta)[n0 + tid % NS];
+  __syncthreads();
+
+  const int kmax = ws_runs_kmax(ntile, nr, tpu);
+  if (wid < NRW) {
+    // ======================= row waves =======================
+    if constexpr ((CTN_DV8_PRIO & 3) != 0) __builtin_amdgcn_s_setprio(CTN_DV8_PRIO & 3);
+    const int r = wid & 3, rb = wid >> 2;
+    v4u wf[2][KB];
+    const bf16raw* WF = reinterpret_cast<const bf16raw*>(p.Wf);
+    const bf16raw* W = reinterpret_cast<const bf16raw*>(p.W);
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const int n = n0 + 32 * r + (lr >> 2) * 8 + nb * 4 + (lr & 3);
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb)
+        wf[nb][kb] = WF ? ldg16(WF + frag_offset(4 * sl + r, nb, kb, lane, KR))
+                        : ldg16(W + (size_t)n * p.ldw + kb * 32 + lg * 8);
+    }
+    const int cl = 32 * r + 8 * lg;
+    bf16raw* Cg = reinterpret_cast<bf16raw*>(p.C);
+    float gam[8];
+    *reinterpret_cast<float4*>(gam) = *reinterpret_cast<const float4*>(p.gamma + n0 + cl);
+    *reinterpret_cast<float4*>(gam + 4) = *reinterpret_cast<const float4*>(p.gamma + n0 + cl + 4);
+    const int abase = rb * KB * 1024 + lg * 256 + ((lr ^ ((lg & 1) * 12)) << 4);   // + kb * 1024
+    const int ro = OFF_B + dv_rbgr(lr, 4 * r + lg) + rb * 4096;                   // raw d, row 16 rb + lr
+    const float eal = p.alpha[0];
+    double run_s = 0.0, run_q = 0.0;
+    const int m0 = t0 / tpu;
+    int run_m = m0;
+    double2* run_slab = p.grp_slab + (((size_t)rr * S + sl) * NRW + wid) * kmax;
+    auto flush = [&]() __attribute__((always_inline)) {
+      const double a = wave_sum_dpp_d(run_s), b = wave_sum_dpp_d(run_q);
+      run_slab[run_m - m0] = make_double2(a, b);
+    };
+    auto run = [&](auto le1) __attribute__((always_inline)) {
+      constexpr bool LE1 = decltype(le1)::value;
+      int slot = 0;
+      uint32_t gen = 1;
+      for (int t = t0; t < t1; ++t) {
+        dv_wait<NCW>(fl_full[slot], gen, p.err);
+        const char* base = smem + slot * SLOT;
+        f32x4_t acc[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+        constexpr int LA = CTN_DV8_LA;
+        v4u bw[LA + 1];
+#pragma unroll
+        for (int kb = 0; kb < LA && kb < KB; ++kb) bw[kb] = *reinterpret_cast<const v4u*>(base + OFF_A + abase + kb * 1024);
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) {
+          if (kb + LA < KB)
+            bw[(kb + LA) % (LA + 1)] = *reinterpret_cast<const v4u*>(base + OFF_A + abase + (kb + LA) * 1024);
+          const v4u b = bw[kb % (LA + 1)];
+#pragma unroll
+          for (int nb = 0; nb < 2; ++nb)
+            acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wf[nb][kb]),
+                                                              __builtin_bit_cast(bf16x8_t, b), acc[nb], 0, 0, 0);
+        }
+        if constexpr (LA > 0) {
+          __builtin_amdgcn_sched_group_barrier(0x100, LA < KB ? LA : KB, 0);
+#pragma unroll
+          for (int kb = 0; kb < KB; ++kb) {
+            if (kb + LA < KB) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+          }
+        }
+        // epilogue: norm-2 backward sums over this wave's 32 channels x 16 rows, C rows
+        const v4u rw = *reinterpret_cast<const v4u*>(base + ro);
+        const float2 est = *reinterpret_cast<const float2*>(base + OFF_ST);   // the tile's utterance
+        const float rs = est.y, ms = -est.x * est.y;
+        float f[8];
+        unpack_bf16x8(rw, f);
+        float s1 = 0.f, q1 = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float a = dv_prelu<LE1>(f[e], eal);
+          const float ah = fmaf(a, rs, ms);
+          const float ga = acc[e >> 2][e & 3] * gam[e];
+          s1 += ga;
+          q1 = fmaf(ga, ah, q1);
+        }
+        const v4u cv = {pk_bf16(acc[0][0], acc[0][1]), pk_bf16(acc[0][2], acc[0][3]), pk_bf16(acc[1][0], acc[1][1]),
+                        pk_bf16(acc[1][2], acc[1][3])};
+        stg16h<CTN_DV_NT != 0>(Cg + (size_t)t * TM * p.ldc + n0 + (uint32_t)((16 * rb + lr) * p.ldc + cl), cv);
+        const int m = t / tpu;
+        if (m != run_m) {
+          flush();
+          run_s = run_q = 0.0;
+          run_m = m;
+        }
+        run_s += (double)s1;
+        run_q += (double)q1;
+        dv_signal(&fl_done[slot][wid], gen);
+        if (++slot == NSL) {
+          slot = 0;
+          ++gen;
+        }
+      }
+    };
+    if (t0 < t1) {
+      if (eal <= 1.f) run(std::true_type{});
+      else run(std::false_type{});
+      flush();
+    }
+    return;
+  }
+  // ======================= column waves (+ the tile DMA) =======================
+  if constexpr ((CTN_DV8_PRIO >> 2 & 3) != 0) __builtin_amdgcn_s_setprio(CTN_DV8_PRIO >> 2 & 3);
+  const int c = wid - NRW;
+  constexpr int CI = 16;   // all 16 row blocks of the dW2 slice x column block c (the CJ = 1 split)
+  f32x4_t dacc[CI];
+#pragma unroll
+  for (int i = 0; i < CI; ++i) dacc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int q = lr >> 2, pp = lr & 3;
+  int abase[2], bbase[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = 8 * lg + 4 * h + q;
+    abase[h] = (lg >> 1) * KB * 1024 + (pp >> 1) * 256 + (((row & 15) ^ ((pp >> 1) * 12)) << 4) + (pp & 1) * 8;
+    bbase[h] = dv_rbgr(row, 2 * c + (pp >> 1)) + 8 * (pp & 1);
+  }
+  const float cg = sgb[0][16 * c + lr], cb = sgb[1][16 * c + lr];
+  const float bal = p.bop.alpha[0];
+  // the DMA share: A pieces f = 2c, 2c + 1 (16 rows x 32 channels of gy each), raw-d piece c
+  // (4 rows x the slice's 128 channels), and (c = 0) the tile's statistics pair
+  const rsrc_t rA = du_rsrc(p.A, rows * p.lda * 2), rD = du_rsrc(p.Bm, rows * p.ldb * 2);
+  const rsrc_t rS = du_rsrc(p.bop.stats, (long)p.g.M * 8);
+  int arow[2];
+  uint32_t aoff[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int f = 2 * c + u, mb = f / KB, kb = f % KB;
+    arow[u] = 16 * mb + ((lane & 15) ^ (((lane >> 4) & 1) * 12));
+    aoff[u] = (uint32_t)(arow[u] * p.lda + (4 * kb + (lane >> 4)) * 8) * 2u;
+  }
+  const int drow = 4 * c + (lane >> 4);
+  uint32_t doff;
+  {
+    const int ps = lane & 15;
+    const int dgr = (ps & 1) | ((((ps >> 1) ^ dv_rbhash(drow)) & 7) << 1);
+    doff = (uint32_t)(drow * p.ldb + n0 + 8 * dgr) * 2u;
+  }
+  const bool st_wave = c == 0;
+  const uint32_t soff = lane < 2 ? (uint32_t)(lane * 4) : DU_OOB;
+  auto dma = [&](int t) __attribute__((always_inline)) {
+    char* base = smem + ((t - t0) % NSL) * SLOT;
+    const int tk = (t * TM) % Kp;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      du_dma16(rA, base + OFF_A + (2 * c + u) * 1024, tk + arow[u] < Kv ? aoff[u] : DU_OOB, t * TM * p.lda * 2);
+    du_dma16(rD, base + OFF_B + c * 1024, doff, t * TM * p.ldb * 2);
+    if (st_wave) du_dma4(rS, base + OFF_ST, soff, (t / tpu) * 8);
+  };
+  auto run = [&](auto le1) __attribute__((always_inline)) {
+    constexpr bool LE1 = decltype(le1)::value;
+    for (int i = 0; i < PF; ++i)
+      if (t0 + i < t1) dma(t0 + i);
+    int slot = 0;
+    uint32_t gen = 1;
+    for (int t = t0; t < t1; ++t) {
+      // this wave's share of tile t landed (the later tiles' shares may stay in flight)
+      if (t1 - 1 - t >= PF - 1) {
+        if (st_wave) dv_vmwait_c<4 * (PF - 1)>();
+        else dv_vmwait_c<3 * (PF - 1)>();
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      dv_signal(&fl_full[slot][c], gen);
+      dv_wait<NCW>(fl_full[slot], gen, p.err);
+      const char* base = smem + slot * SLOT;
+      // B fragment: raw d of column 16c + lr (slice-local), frame rows 8lg .. 8lg+7 -> op(d)
+      const s16x4_t lo = dv_tr(base + OFF_B + bbase[0]);
+      const s16x4_t hi = dv_tr(base + OFF_B + bbase[1]);
+      v4u v = __builtin_bit_cast(v4u, bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+      {
+        const float2 st = *reinterpret_cast<const float2*>(base + OFF_ST);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float x0 = __uint_as_float(v[k] << 16), x1 = __uint_as_float(v[k] & 0xffff0000u);
+          x0 = dv_prelu<LE1>(x0, bal);
+          x1 = dv_prelu<LE1>(x1, bal);
+          x0 = fmaf(x0 - st.x, st.y * cg, cb);
+          x1 = fmaf(x1 - st.x, st.y * cg, cb);
+          v[k] = pk_bf16(x0, x1);
+        }
+      }
+      const bf16x8_t bfr = __builtin_bit_cast(bf16x8_t, v);
+#pragma unroll
+      for (int i = 0; i < CI; ++i) {
+        const int o = (i >> 1) * 1024 + (i & 1) * 512;
+        const s16x4_t alo = dv_tr(base + OFF_A + abase[0] + o), ahi = dv_tr(base + OFF_A + abase[1] + o);
+        const bf16x8_t af = bf16x8_t{alo[0], alo[1], alo[2], alo[3], ahi[0], ahi[1], ahi[2], ahi[3]};
+        dacc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, dacc[i], 0, 0, 0);
+      }
+      dv_signal(&fl_done[slot][NRW + c], gen);
+      const int tn = t + PF;
+      if (tn < t1) {
+        const int kn = tn - t0;   // its slot was last used by tile tn - NSL (= t - 1): every DONE of it
+        dv_wait<NRW + NCW>(fl_done[kn % NSL], (uint32_t)(kn / NSL), p.err);
+        dma(tn);
+      }
+      if (++slot == NSL) {
+        slot = 0;
+        ++gen;
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  if (t0 < t1) {
+    if (bal <= 1.f) run(std::true_type{});
+    else run(std::false_type{});
+  }
+  // dW2 partial of this workgroup: lane holds D[i*16 + 4lg + e][n0 + 16c + lr]
+  float* Dp = p.Dpart + (size_t)rr * KR * p.Nout;
+  const int n = n0 + 16 * c + lr;
+#pragma unroll
+  for (int i = 0; i < CI; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) st_part<CTN_PART_NT != 0>(&Dp[(size_t)(i * 16 + 4 * lg + e) * p.Nout + n], dacc[i][e]);
 }
 
 }  // namespace
@@ -867,6 +1195,20 @@ bool gemm_dual_ws_enabled() {
 
 // cLN statistics entries per (row, slice) the kernel stores (gemm_dual_group_parts)
 int dual_ws_cln_parts_per_slice() { return CTN_DV_CLNC ? 1 : DV_NR; }
+
+// The gLN form on gemm_dual_r8_kernel (eight row waves, the tile DMA in the column
+// waves): CTN_DUAL_R8=1 (experiment; read on every query).  Bit-identical C and dW2, but
+// measured slower: 95-120 us against 75-79 us for the four-row-wave kernel at the bench
+// shape (microbenchmark, round 6) — without dedicated high-priority memory
+// waves the DMA issue waits behind the column waves' MFMA work and the ring runs dry.
+static bool dual_r8(const GemmDual& p) {
+  if (p.norm != NORM_GLN) return false;
+  const char* e = getenv("CTN_DUAL_R8");
+  return e ? atoi(e) != 0 : false;
+}
+// row waves per slice of the wave-specialised kernel that runs p (its gLN statistics
+// partials are per (range, slice, row wave): gemm_dual_runs)
+int dual_ws_row_waves(const GemmDual& p) { return dual_r8(p) ? 8 : DV_NR; }
 
 bool gemm_dual_ws_eligible(const GemmDual& p) {
   if (!gemm_dual_ws_enabled()) return false;
@@ -933,7 +1275,9 @@ hipError_t launch_gemm_dual_ws(const GemmDual& pa, hipStream_t s) {
   GemmDual p = pa;
   p.err = device_error_word();
   const dim3 grid(gemm_dual_ws_ranges(p) * (p.Nout / DV_NS));
-  if (p.norm == NORM_GLN)
+  if (p.norm == NORM_GLN && dual_r8(p))
+    hipLaunchKernelGGL((gemm_dual_r8_kernel<DV_NSL, DV_PF>), grid, dim3(1024), 0, s, p);
+  else if (p.norm == NORM_GLN)
     hipLaunchKernelGGL((gemm_dual_ws_kernel<NORM_GLN, DV_NSL, DV_PF>), grid, dim3(DV_NT), 0, s, p);
   else
     hipLaunchKernelGGL((gemm_dual_ws_kernel<NORM_CLN, DV_NSL, DV_PF_CLN>), grid, dim3(DV_NT), 0, s, p);

@@ -635,7 +635,7 @@ WsRuns gemm_dual_runs(const GemmDual& p) {
   w.ntile = (int)(p.g.rows() / DU_TM);
   w.grid = gemm_dual_ranges(p);
   w.tpu = p.g.Kp / DU_TM;
-  w.waves = dual_slices(p) * (gemm_dual_ws_eligible(p) ? 4 : DU_WV);   // ctn_dual_ws.hip: 4 row waves
+  w.waves = dual_slices(p) * (gemm_dual_ws_eligible(p) ? dual_ws_row_waves(p) : DU_WV);   // ctn_dual_ws.hip
   w.kmax = ws_runs_kmax(w.ntile, w.grid, w.tpu);
   return w;
 }

@@ -124,6 +124,7 @@ bool gemm_dual_eligible(DType dt, const GemmDual& p);
 int gemm_dual_ranges(const GemmDual& p);
 int gemm_dual_group_parts(const GemmDual& p);
 int dual_ws_cln_parts_per_slice();   // ctn_dual_ws.hip: cLN statistics entries per (row, slice)
+int dual_ws_row_waves(const GemmDual& p);   // ctn_dual_ws.hip: row waves per slice (gLN partials)
 StatFold gemm_dual_stat_fold(const GemmDual& p, const double2* slab, double cnt, float eps, int mode,
                              float2* out);
 hipError_t launch_gemm_dual(const GemmDual& p, hipStream_t s);

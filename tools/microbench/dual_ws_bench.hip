@@ -221,6 +221,31 @@ int main(int argc, char** argv) {
     printf("EXP %d %-4s M=%d K=%d %s %8.1f us  %7.0f GB/s (alg. bytes)\n", CTN_DV_EXP, ws ? "ws" : "old", M, K,
            NK == NORM_GLN ? "gLN" : "cLN", us, bytes / us * 1e-3);
   }
+#if CTN_DV_STAMP
+  {   // per-role wait shares of the wave-specialised kernel (one more launch, stamps zeroed)
+    std::vector<unsigned long long> h(1024 * 16 * 4, 0ull);
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(dv_stamps), h.data(), h.size() * 8));
+    setenv("CTN_DUAL_WS", "1", 1);
+    CK(launch_gemm_dual(g, 0));
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(dv_stamps), h.size() * 8));
+    const int nwg = gemm_dual_ws_ranges(g) * (H / 128);
+    const char* role[3] = {"row", "column", "memory"};
+    for (int r = 0; r < 3; ++r) {
+      double acc[4] = {0, 0, 0, 0};
+      int n = 0;
+      for (int b = 0; b < nwg; ++b)
+        for (int w = 0; w < 16; ++w) {
+          const int rr = w < 4 ? 0 : w < 12 ? 1 : 2;
+          if (rr != r) continue;
+          ++n;
+          for (int i = 0; i < 4; ++i) acc[i] += (double)h[((size_t)b * 16 + w) * 4 + i];
+        }
+      printf("STAMP %-6s loop %8.0f cyc  full-wait %5.1f%%  dma-vmcnt %5.1f%%  done-wait %5.1f%%\n", role[r],
+             acc[3] / n, 100 * acc[0] / acc[3], 100 * acc[1] / acc[3], 100 * acc[2] / acc[3]);
+    }
+  }
+#endif
   // the same kernel's COLS mode (dW1 = gh1^T . x shape: A = d [rows][H], B = gy [rows][B])
   {
     GemmCols c{};
