@@ -182,7 +182,10 @@ build/dv6_%: tools/microbench/dual_ws_bench.hip $(PKG)/csrc/ctn_dual_ws.hip $(PK
 # round 6: WS GEMM variants by -D flags: build/ws6_<name> from WS6_<name>
 WS6_base :=
 WS6_pp := -DCTN_WS_PP=1
-WS6_NAMES := base pp
+WS6_la1 := -DCTN_WS_LA16=1
+WS6_la2 := -DCTN_WS_LA16=2
+WS6_pr := -DCTN_WS_PRIO=1
+WS6_NAMES := base pp la1 la2 pr
 ws6: $(patsubst %,build/ws6_%,$(WS6_NAMES))
 build/ws6_%: tools/microbench/ws_bench.hip $(PKG)/csrc/ctn_gemm_ws.hip $(HDR)
 	@mkdir -p build

@@ -84,8 +84,11 @@ constexpr int WS_FOLD_MAX = 512;   // utterances whose gLN operand stats a workg
 #define CTN_WS_S512 1
 #endif
 // LDS fragment look-ahead of the MFMA loop, in k-steps
+// (16 waves: plain-operand configurations only; 1 = one k-step ahead, 124 VGPRs without
+// spills for the forward B -> H GEMM: 36.1 -> 34.5 us, microbenchmark, round 6; the
+// transformed-operand 16-wave configurations spill more with it)
 #ifndef CTN_WS_LA16
-#define CTN_WS_LA16 0
+#define CTN_WS_LA16 1
 #endif
 #ifndef CTN_WS_LA8
 #define CTN_WS_LA8 3
@@ -445,7 +448,7 @@ __global__ __launch_bounds__(64 * WV, (S == 2 ? 2 : 1) * WV / 4) void gemm_ws_ke
   // LDS fragment reads run LA k-steps ahead of the MFMAs that consume them (a
   // register window of LA+1 steps), so a k-step's MFMAs never wait on a read issued
   // just before them (one read in flight per step exposed the LDS latency 16x/tile).
-  constexpr int LA = SWP ? 0 : WV == 16 ? CTN_WS_LA16 : CTN_WS_LA8;
+  constexpr int LA = SWP ? 0 : WV == 16 ? (OPK == OP_PLAIN ? CTN_WS_LA16 : 0) : CTN_WS_LA8;
   auto mfma_tile = [&](const char* buf, f32x4_t (&acc)[MB][NB]) __attribute__((always_inline)) {
     if constexpr (CTN_WS_PRIO) __builtin_amdgcn_s_setprio(1);   // experiment: MFMA issue first
 #pragma unroll
