@@ -157,22 +157,7 @@ DV6_st := -DCTN_DV_STAMP=1
 DV6_st2 := -DCTN_DV_STAMP=1 -DCTN_DV_EXP=2
 DV6_st64 := -DCTN_DV_STAMP=1 -DCTN_DV_EXP=64
 DV6_st0 := -DCTN_DV_STAMP=1 -DCTN_DV_PRIO=0
-DV6_r8p0 := -DCTN_DV8_PRIO=0
-DV6_r8p4 := -DCTN_DV8_PRIO=4
-DV6_r8p9 := -DCTN_DV8_PRIO=9
-DV6_r8p8 := -DCTN_DV8_PRIO=8
-DV6_r8la1 := -DCTN_DV8_LA=1
-DV6_r8la3 := -DCTN_DV8_LA=3
-DV6_mst := -DCTN_DV_STAMP=1
-DV6_mp33 := -DCTN_DV_PRIO=33
-DV6_mp17 := -DCTN_DV_PRIO=17
-DV6_mp1 := -DCTN_DV_PRIO=1
-DV6_mp48 := -DCTN_DV_PRIO=48
-DV6_mp0 := -DCTN_DV_PRIO=0
-DV6_mp50 := -DCTN_DV_PRIO=50
-DV6_mpf3 := -DCTN_DVM_PF=3
-DV6_mpf2 := -DCTN_DVM_PF=2
-DV6_NAMES := mst mp33 mp17 mp1 mp48 mp0 mp50 mpf3 mpf2 r8p0 r8p4 r8p9 r8p8 r8la1 r8la3 st st2 st64 st0 e1 e2 e64 e32 e34 e96 e4 e8 la2 pf4 pf3 nc4 la0 base p0 prow pcol pmem pmem2 partnt0 clnc0 p17 p18 p33 p48 p20 p34 p49 p50 p37
+DV6_NAMES := st st2 st64 st0 e1 e2 e64 e32 e34 e96 e4 e8 la2 pf4 pf3 nc4 la0 base p0 prow pcol pmem pmem2 partnt0 clnc0 p17 p18 p33 p48 p20 p34 p49 p50 p37
 dv6: $(patsubst %,build/dv6_%,$(DV6_NAMES))
 build/dv6_%: tools/microbench/dual_ws_bench.hip $(PKG)/csrc/ctn_dual_ws.hip $(PKG)/csrc/ctn_gemm_dual.hip $(HDR)
 	@mkdir -p build

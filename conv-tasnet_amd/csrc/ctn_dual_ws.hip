@@ -152,15 +152,6 @@ template <int SHIFT, int NK> CTN_DEV void dv_prio() {
   if constexpr (pr != 0) __builtin_amdgcn_s_setprio(pr);
 }
 
-// gemm_dual_r8_kernel (gLN): static priorities (bits 0-1 row waves, 2-3 column waves) and
-// the row waves' A-fragment look-ahead
-#ifndef CTN_DV8_PRIO
-#define CTN_DV8_PRIO 1
-#endif
-#ifndef CTN_DV8_LA
-#define CTN_DV8_LA 2
-#endif
-
 // Row waves: A fragments read LA k-steps ahead of their MFMAs
 #ifndef CTN_DV_LA
 #define CTN_DV_LA 1
@@ -913,653 +904,6 @@ __global__ __launch_bounds__(COLS ? (DV_NC + DV_NMW) * 64 : DV_NT) void gemm_dua
   }
 }
 
-// ---------------------------------------------------------------------------
-// gLN form with eight row waves (CTN_DUAL_R8, round 6).  Wait stamps of the kernel above
-// (CTN_DV_STAMP) put its critical path in the row waves: busy 84 % of
-// their loop against 64 % for the column waves, while the memory waves idle 55 % waiting
-// for the consumers.  Here the row GEMM of a tile is split by row block over two waves per
-// SIMD (wave (r, rb): output channels n0 + 32r .. +31, frame rows 16rb .. 16rb + 15; same
-// resident W2 fragments, same MFMA sequence per output, so C is bit-identical), and the
-// memory role moves into the column waves, which had the slack: column wave c LDS-DMAs
-// A pieces 2c, 2c + 1, raw-d piece c and (c = 0) the tile's statistics, publishes FULL for
-// its share once its own vmcnt says the share landed, and refills the slot of tile t - 1
-// with tile t + PF after every consumer's DONE of it.  16 waves: 8 row, 8 column.  The
-// norm-2 statistics partials are per (range, slice, row wave): 8 waves per slice
-// (dual_ws_row_waves).
-template <int NSL, int PF>
-__global__ __launch_bounds__(1024) void gemm_dual_r8_kernel(GemmDual p) {
-  constexpr int TM = DV_TM, KB = DV_KB, KR = DV_KR, NS = DV_NS, SLOT = DV_SLOT;
-  constexpr int NRW = 8, NCW = 8;
-  static_assert(DV_RB, "raw-B slot layout");
-  static_assert(NSL * SLOT <= 160 * 1024 - 2048, "LDS budget");
-  __shared__ __attribute__((aligned(16))) char smem[NSL * SLOT];
-  __shared__ __attribute__((aligned(16))) uint32_t fl_full[NSL][NCW];          // per column wave (its DMA share)
-  __shared__ __attribute__((aligned(16))) uint32_t fl_done[NSL][NRW + NCW];    // per consumer
-  __shared__ __attribute__((aligned(16))) float sgb[2][NS];
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lr = lane & 15, lg = lane >> 4;
-  const int S = p.Nout / NS;
-  const int nr = (int)gridDim.x / S;
-  int rr, sl;
-  {
-    const int b = (int)blockIdx.x;
-    if ((int)gridDim.x % (8 * S) == 0) {
-      const int l = b / 8;
-      sl = l % S;
-      rr = (b % 8) * (nr / 8) + l / S;
-    } else {
-      sl = b % S;
-      rr = b / S;
-    }
-  }
-  const long rows = p.g.rows();
-  const int ntile = (int)(rows / TM);
-  const int t0 = (int)((long)ntile * rr / nr), t1 = (int)((long)ntile * (rr + 1) / nr);
-  const int n0 = sl * NS;
-  const int Kp = p.g.Kp, Kv = p.g.K, tpu = Kp / TM;
-
-  if (tid < NSL * NCW) (&fl_full[0][0])[tid] = 0u;
-  else if (tid < NSL * (NCW + NRW + NCW)) (&fl_done[0][0])[tid - NSL * NCW] = 0u;
-  if (tid < 2 * NS) sgb[tid / NS][tid % NS] = (tid < NS ? p.bop.gamma : p.bop.beta)[n0 + tid % NS];
-  __syncthreads();
-
-  const int kmax = ws_runs_kmax(ntile, nr, tpu);
-  if (wid < NRW) {
-    // ======================= row waves =======================
-    if constexpr ((CTN_DV8_PRIO & 3) != 0) __builtin_amdgcn_s_setprio(CTN_DV8_PRIO & 3);
-    const int r = wid & 3, rb = wid >> 2;
-    v4u wf[2][KB];
-    const bf16raw* WF = reinterpret_cast<const bf16raw*>(p.Wf);
-    const bf16raw* W = reinterpret_cast<const bf16raw*>(p.W);
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {
-      const int n = n0 + 32 * r + (lr >> 2) * 8 + nb * 4 + (lr & 3);
-#pragma unroll
-      for (int kb = 0; kb < KB; ++kb)
-        wf[nb][kb] = WF ? ldg16(WF + frag_offset(4 * sl + r, nb, kb, lane, KR))
-                        : ldg16(W + (size_t)n * p.ldw + kb * 32 + lg * 8);
-    }
-    const int cl = 32 * r + 8 * lg;
-    bf16raw* Cg = reinterpret_cast<bf16raw*>(p.C);
-    float gam[8];
-    *reinterpret_cast<float4*>(gam) = *reinterpret_cast<const float4*>(p.gamma + n0 + cl);
-    *reinterpret_cast<float4*>(gam + 4) = *reinterpret_cast<const float4*>(p.gamma + n0 + cl + 4);
-    const int abase = rb * KB * 1024 + lg * 256 + ((lr ^ ((lg & 1) * 12)) << 4);   // + kb * 1024
-    const int ro = OFF_B + dv_rbgr(lr, 4 * r + lg) + rb * 4096;                   // raw d, row 16 rb + lr
-    const float eal = p.alpha[0];
-    double run_s = 0.0, run_q = 0.0;
-    const int m0 = t0 / tpu;
-    int run_m = m0;
-    double2* run_slab = p.grp_slab + (((size_t)rr * S + sl) * NRW + wid) * kmax;
-    auto flush = [&]() __attribute__((always_inline)) {
-      const double a = wave_sum_dpp_d(run_s), b = wave_sum_dpp_d(run_q);
-      run_slab[run_m - m0] = make_double2(a, b);
-    };
-    auto run = [&](auto le1) __attribute__((always_inline)) {
-      constexpr bool LE1 = decltype(le1)::value;
-      int slot = 0;
-      uint32_t gen = 1;
-      for (int t = t0; t < t1; ++t) {
-        dv_wait<NCW>(fl_full[slot], gen, p.err);
-        const char* base = smem + slot * SLOT;
-        f32x4_t acc[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
-        constexpr int LA = CTN_DV8_LA;
-        v4u bw[LA + 1];
-#pragma unroll
-        for (int kb = 0; kb < LA && kb < KB; ++kb) bw[kb] = *reinterpret_cast<const v4u*>(base + OFF_A + abase + kb * 1024);
-#pragma unroll
-        for (int kb = 0; kb < KB; ++kb) {
-          if (kb + LA < KB)
-            bw[(kb + LA) % (LA + 1)] = *reinterpret_cast<const v4u*>(base + OFF_A + abase + (kb + LA) * 1024);
-          const v4u b = bw[kb % (LA + 1)];
-#pragma unroll
-          for (int nb = 0; nb < 2; ++nb)
-            acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wf[nb][kb]),
-                                                              __builtin_bit_cast(bf16x8_t, b), acc[nb], 0, 0, 0);
-        }
-        if constexpr (LA > 0) {
-          __builtin_amdgcn_sched_group_barrier(0x100, LA < KB ? LA : KB, 0);
-#pragma unroll
-          for (int kb = 0; kb < KB; ++kb) {
-            if (kb + LA < KB) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-          }
-        }
-        // epilogue: norm-2 backward sums over this wave's 32 channels x 16 rows, C rows
-        const v4u rw = *reinterpret_cast<const v4u*>(base + ro);
-        const float2 est = *reinterpret_cast<const float2*>(base + OFF_ST);   // the tile's utterance
-        const float rs = est.y, ms = -est.x * est.y;
-        float f[8];
-        unpack_bf16x8(rw, f);
-        float s1 = 0.f, q1 = 0.f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float a = dv_prelu<LE1>(f[e], eal);
-          const float ah = fmaf(a, rs, ms);
-          const float ga = acc[e >> 2][e & 3] * gam[e];
-          s1 += ga;
-          q1 = fmaf(ga, ah, q1);
-        }
-        const v4u cv = {pk_bf16(acc[0][0], acc[0][1]), pk_bf16(acc[0][2], acc[0][3]), pk_bf16(acc[1][0], acc[1][1]),
-                        pk_bf16(acc[1][2], acc[1][3])};
-        stg16h<CTN_DV_NT != 0>(Cg + (size_t)t * TM * p.ldc + n0 + (uint32_t)((16 * rb + lr) * p.ldc + cl), cv);
-        const int m = t / tpu;
-        if (m != run_m) {
-          flush();
-          run_s = run_q = 0.0;
-          run_m = m;
-        }
-        run_s += (double)s1;
-        run_q += (double)q1;
-        dv_signal(&fl_done[slot][wid], gen);
-        if (++slot == NSL) {
-          slot = 0;
-          ++gen;
-        }
-      }
-    };
-    if (t0 < t1) {
-      if (eal <= 1.f) run(std::true_type{});
-      else run(std::false_type{});
-      flush();
-    }
-    return;
-  }
-  // ======================= column waves (+ the tile DMA) =======================
-  if constexpr ((CTN_DV8_PRIO >> 2 & 3) != 0) __builtin_amdgcn_s_setprio(CTN_DV8_PRIO >> 2 & 3);
-  const int c = wid - NRW;
-  constexpr int CI = 16;   // all 16 row blocks of the dW2 slice x column block c (the CJ = 1 split)
-  f32x4_t dacc[CI];
-#pragma unroll
-  for (int i = 0; i < CI; ++i) dacc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  const int q = lr >> 2, pp = lr & 3;
-  int abase[2], bbase[2];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int row = 8 * lg + 4 * h + q;
-    abase[h] = (lg >> 1) * KB * 1024 + (pp >> 1) * 256 + (((row & 15) ^ ((pp >> 1) * 12)) << 4) + (pp & 1) * 8;
-    bbase[h] = dv_rbgr(row, 2 * c + (pp >> 1)) + 8 * (pp & 1);
-  }
-  const float cg = sgb[0][16 * c + lr], cb = sgb[1][16 * c + lr];
-  const float bal = p.bop.alpha[0];
-  // the DMA share: A pieces f = 2c, 2c + 1 (16 rows x 32 channels of gy each), raw-d piece c
-  // (4 rows x the slice's 128 channels), and (c = 0) the tile's statistics pair
-  const rsrc_t rA = du_rsrc(p.A, rows * p.lda * 2), rD = du_rsrc(p.Bm, rows * p.ldb * 2);
-  const rsrc_t rS = du_rsrc(p.bop.stats, (long)p.g.M * 8);
-  int arow[2];
-  uint32_t aoff[2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int f = 2 * c + u, mb = f / KB, kb = f % KB;
-    arow[u] = 16 * mb + ((lane & 15) ^ (((lane >> 4) & 1) * 12));
-    aoff[u] = (uint32_t)(arow[u] * p.lda + (4 * kb + (lane >> 4)) * 8) * 2u;
-  }
-  const int drow = 4 * c + (lane >> 4);
-  uint32_t doff;
-  {
-    const int ps = lane & 15;
-    const int dgr = (ps & 1) | ((((ps >> 1) ^ dv_rbhash(drow)) & 7) << 1);
-    doff = (uint32_t)(drow * p.ldb + n0 + 8 * dgr) * 2u;
-  }
-  const bool st_wave = c == 0;
-  const uint32_t soff = lane < 2 ? (uint32_t)(lane * 4) : DU_OOB;
-  auto dma = [&](int t) __attribute__((always_inline)) {
-    char* base = smem + ((t - t0) % NSL) * SLOT;
-    const int tk = (t * TM) % Kp;
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-      du_dma16(rA, base + OFF_A + (2 * c + u) * 1024, tk + arow[u] < Kv ? aoff[u] : DU_OOB, t * TM * p.lda * 2);
-    du_dma16(rD, base + OFF_B + c * 1024, doff, t * TM * p.ldb * 2);
-    if (st_wave) du_dma4(rS, base + OFF_ST, soff, (t / tpu) * 8);
-  };
-  auto run = [&](auto le1) __attribute__((always_inline)) {
-    constexpr bool LE1 = decltype(le1)::value;
-    for (int i = 0; i < PF; ++i)
-      if (t0 + i < t1) dma(t0 + i);
-    int slot = 0;
-    uint32_t gen = 1;
-    for (int t = t0; t < t1; ++t) {
-      // this wave's share of tile t landed (the later tiles' shares may stay in flight)
-      if (t1 - 1 - t >= PF - 1) {
-        if (st_wave) dv_vmwait_c<4 * (PF - 1)>();
-        else dv_vmwait_c<3 * (PF - 1)>();
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      dv_signal(&fl_full[slot][c], gen);
-      dv_wait<NCW>(fl_full[slot], gen, p.err);
-      const char* base = smem + slot * SLOT;
-      // B fragment: raw d of column 16c + lr (slice-local), frame rows 8lg .. 8lg+7 -> op(d)
-      const s16x4_t lo = dv_tr(base + OFF_B + bbase[0]);
-      const s16x4_t hi = dv_tr(base + OFF_B + bbase[1]);
-      v4u v = __builtin_bit_cast(v4u, bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
-      {
-        const float2 st = *reinterpret_cast<const float2*>(base + OFF_ST);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          float x0 = __uint_as_float(v[k] << 16), x1 = __uint_as_float(v[k] & 0xffff0000u);
-          x0 = dv_prelu<LE1>(x0, bal);
-          x1 = dv_prelu<LE1>(x1, bal);
-          x0 = fmaf(x0 - st.x, st.y * cg, cb);
-          x1 = fmaf(x1 - st.x, st.y * cg, cb);
-          v[k] = pk_bf16(x0, x1);
-        }
-      }
-      const bf16x8_t bfr = __builtin_bit_cast(bf16x8_t, v);
-#pragma unroll
-      for (int i = 0; i < CI; ++i) {
-        const int o = (i >> 1) * 1024 + (i & 1) * 512;
-        const s16x4_t alo = dv_tr(base + OFF_A + abase[0] + o), ahi = dv_tr(base + OFF_A + abase[1] + o);
-        const bf16x8_t af = bf16x8_t{alo[0], alo[1], alo[2], alo[3], ahi[0], ahi[1], ahi[2], ahi[3]};
-        dacc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, dacc[i], 0, 0, 0);
-      }
-      dv_signal(&fl_done[slot][NRW + c], gen);
-      const int tn = t + PF;
-      if (tn < t1) {
-        const int kn = tn - t0;   // its slot was last used by tile tn - NSL (= t - 1): every DONE of it
-        dv_wait<NRW + NCW>(fl_done[kn % NSL], (uint32_t)(kn / NSL), p.err);
-        dma(tn);
-      }
-      if (++slot == NSL) {
-        slot = 0;
-        ++gen;
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  };
-  if (t0 < t1) {
-    if (bal <= 1.f) run(std::true_type{});
-    else run(std::false_type{});
-  }
-  // dW2 partial of this workgroup: lane holds D[i*16 + 4lg + e][n0 + 16c + lr]
-  float* Dp = p.Dpart + (size_t)rr * KR * p.Nout;
-  const int n = n0 + 16 * c + lr;
-#pragma unroll
-  for (int i = 0; i < CI; ++i)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) st_part<CTN_PART_NT != 0>(&Dp[(size_t)(i * 16 + 4 * lg + e) * p.Nout + n], dacc[i][e]);
-}
-
-// ---------------------------------------------------------------------------
-// gLN form with the row epilogue in the memory waves (CTN_DUAL_ME, round 6).  The wait
-// stamps of gemm_dual_ws_kernel put its critical path in the row waves (busy 84 % of
-// their loop) while the memory waves idle 55 % waiting for DONE, and the bound-finding
-// build without epilogue arithmetic ran 13 % faster.  Here a row wave
-// runs only the tile's MFMAs and parks its fp32 accumulators in an LDS staging buffer
-// (two tiles deep, 4 KB per wave and tile); memory wave m (same SIMD as row wave m) runs
-// that wave's epilogue — norm-2 backward sums from the same fp32 values in the same order,
-// C stores — after publishing FULL of the next tile, and publishes the row role's DONE of
-// the slot (the epilogue reads raw d from it).  C, dW2 and the statistics are
-// bit-identical to gemm_dual_ws_kernel.  Ring of NSL slots (5: the staging buffer takes
-// the sixth slot's LDS).  Measured slower (microbenchmark, bench shape, one box: 84-91 us
-// against 74-79 us): the memory waves' LDS-DMA issue (~100 cycles per
-// piece) plus the epilogue make them the critical path (row waves wait for FULL 46 %).
-constexpr bool DV_ME_OK = DV_RB && !DV_NI && DV_CJ == 1 && DV_NC == 8;   // the layout it is written for
-#ifndef CTN_DVM_NSL
-#define CTN_DVM_NSL 5
-#endif
-#ifndef CTN_DVM_PF
-#define CTN_DVM_PF (CTN_DVM_NSL - 2)
-#endif
-// one generation word (per-wave hand-off)
-CTN_DEV void dv_wait1(const uint32_t* f, uint32_t gen, uint32_t* err) {
-  uint32_t it = 0;
-  for (; it < CTN_SPIN_LIMIT; ++it) {
-    const uint32_t v = *(const lds_u32*)(f);
-    if (__builtin_amdgcn_readfirstlane(v) >= gen) break;
-    __builtin_amdgcn_s_sleep(1);
-  }
-  if (it == CTN_SPIN_LIMIT) spin_timeout(err);
-  asm volatile("" ::: "memory");
-}
-
-template <int NSL, int PF>
-__global__ __launch_bounds__(DV_NT) void gemm_dual_me_kernel(GemmDual p) {
-  constexpr int TM = DV_TM, KB = DV_KB, KR = DV_KR, NS = DV_NS, SLOT = DV_SLOT;
-  constexpr int NR = DV_NR, ND = DV_NR + DV_NC, CI = 16 * 8 / DV_NC;
-  constexpr int EW = 64 * 16;   // staged floats per row wave and tile
-  static_assert(DV_ME_OK, "raw-B slot layout, eight column waves of one column block");
-  static_assert(NSL * SLOT + 2 * NR * EW * 4 <= 160 * 1024 - 2048, "LDS budget");
-  static_assert(PF >= 1 && PF <= NSL - 2, "ring look-ahead (the epilogue of tile k - 1 follows the refill)");
-  __shared__ __attribute__((aligned(16))) char smem[NSL * SLOT];
-  __shared__ __attribute__((aligned(16))) float estage[2][NR][EW];
-  __shared__ __attribute__((aligned(16))) uint32_t fl_full[NSL][4];
-  __shared__ __attribute__((aligned(16))) uint32_t fl_done[NSL][ND];   // row role: written by memory wave r
-  __shared__ __attribute__((aligned(16))) uint32_t fl_acc[2][NR];      // row wave r staged tile k (buffer k & 1)
-  __shared__ __attribute__((aligned(16))) uint32_t fl_efree[2][NR];    // memory wave r consumed it
-  __shared__ __attribute__((aligned(16))) float sgb[2][NS];
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lr = lane & 15, lg = lane >> 4;
-  const int S = p.Nout / NS;
-  const int nr = (int)gridDim.x / S;
-  int rr, sl;
-  {
-    const int b = (int)blockIdx.x;
-    if ((int)gridDim.x % (8 * S) == 0) {
-      const int l = b / 8;
-      sl = l % S;
-      rr = (b % 8) * (nr / 8) + l / S;
-    } else {
-      sl = b % S;
-      rr = b / S;
-    }
-  }
-  const long rows = p.g.rows();
-  const int ntile = (int)(rows / TM);
-  const int t0 = (int)((long)ntile * rr / nr), t1 = (int)((long)ntile * (rr + 1) / nr);
-  const int n0 = sl * NS;
-  const int Kp = p.g.Kp, Kv = p.g.K, tpu = Kp / TM;
-
-  if (tid < NSL * 4) (&fl_full[0][0])[tid] = 0u;
-  else if (tid < NSL * (4 + ND)) (&fl_done[0][0])[tid - NSL * 4] = 0u;
-  else if (tid < NSL * (4 + ND) + 2 * NR) (&fl_acc[0][0])[tid - NSL * (4 + ND)] = 0u;
-  else if (tid < NSL * (4 + ND) + 4 * NR) (&fl_efree[0][0])[tid - NSL * (4 + ND) - 2 * NR] = 0u;
-  if (tid >= 1024 - 2 * NS) sgb[(tid - (1024 - 2 * NS)) / NS][tid % NS] = (tid - (1024 - 2 * NS) < NS ? p.bop.gamma : p.bop.beta)[n0 + tid % NS];
-  __syncthreads();
-
-  const int kmax = ws_runs_kmax(ntile, nr, tpu);
-  if (wid < NR) {
-    // ======================= row waves: MFMAs only =======================
-    dv_prio<0, NORM_GLN>();
-    const int r = wid;
-    v4u wf[2][KB];
-    const bf16raw* WF = reinterpret_cast<const bf16raw*>(p.Wf);
-    const bf16raw* W = reinterpret_cast<const bf16raw*>(p.W);
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {
-      const int n = n0 + 32 * r + (lr >> 2) * 8 + nb * 4 + (lr & 3);
-#pragma unroll
-      for (int kb = 0; kb < KB; ++kb)
-        wf[nb][kb] = WF ? ldg16(WF + frag_offset(4 * sl + r, nb, kb, lane, KR))
-                        : ldg16(W + (size_t)n * p.ldw + kb * 32 + lg * 8);
-    }
-    const int rbase = lg * 256 + ((lr ^ ((lg & 1) * 12)) << 4);
-    DV_STAMP_DECL;
-    int slot = 0;
-    uint32_t gen = 1;
-    DV_TS(tl0);
-    for (int t = t0; t < t1; ++t) {
-      const int k = t - t0, eb = k & 1;
-      DV_TS(tw0);
-      dv_wait<4>(fl_full[slot], gen, p.err);
-      DV_ACC(0, tw0);
-      const char* base = smem + slot * SLOT;
-      f32x4_t acc[2][2];
-#pragma unroll
-      for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) acc[rb][nb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      constexpr int LA = DV_LA;
-      v4u bw[LA + 1][2];
-      auto rd = [&](int kb) __attribute__((always_inline)) {
-#pragma unroll
-        for (int rb = 0; rb < 2; ++rb)
-          bw[kb % (LA + 1)][rb] = *reinterpret_cast<const v4u*>(base + OFF_A + rb * KB * 1024 + rbase + kb * 1024);
-      };
-#pragma unroll
-      for (int kb = 0; kb < LA && kb < KB; ++kb) rd(kb);
-#pragma unroll
-      for (int kb = 0; kb < KB; ++kb) {
-        if (kb + LA < KB) rd(kb + LA);
-#pragma unroll
-        for (int rb = 0; rb < 2; ++rb) {
-          const v4u b = bw[kb % (LA + 1)][rb];
-#pragma unroll
-          for (int nb = 0; nb < 2; ++nb)
-            acc[rb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wf[nb][kb]),
-                                                                  __builtin_bit_cast(bf16x8_t, b), acc[rb][nb], 0, 0, 0);
-        }
-      }
-      if constexpr (LA > 0) {
-        __builtin_amdgcn_sched_group_barrier(0x100, 2 * (LA < KB ? LA : KB), 0);
-#pragma unroll
-        for (int kb = 0; kb < KB; ++kb) {
-          if (kb + LA < KB) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-        }
-      }
-      // staging buffer eb was consumed by memory wave r (its epilogue of tile k - 2)
-      DV_TS(te0);
-      if (k >= 2) dv_wait1(&fl_efree[eb][r], (uint32_t)(k >> 1), p.err);
-      DV_ACC(1, te0);
-      float* E = &estage[eb][r][0];
-#pragma unroll
-      for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) *reinterpret_cast<f32x4_t*>(E + (2 * rb + nb) * 256 + lane * 4) = acc[rb][nb];
-      dv_signal(&fl_acc[eb][r], (uint32_t)(k >> 1) + 1u);
-      if (++slot == NSL) {
-        slot = 0;
-        ++gen;
-      }
-    }
-    DV_ACC(3, tl0);
-    DV_STAMP_STORE;
-    return;
-  }
-  if (wid < ND) {
-    // ======================= column waves (gemm_dual_ws_kernel's, CJ = 1) =======================
-    dv_prio<2, NORM_GLN>();
-    const int c = wid - NR, wp = c / 8, wn = c % 8;
-    DV_STAMP_DECL;
-    f32x4_t dacc[CI];
-#pragma unroll
-    for (int i = 0; i < CI; ++i) dacc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    const int q = lr >> 2, pp = lr & 3;
-    int abase[2], bbase[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int row = 8 * lg + 4 * h + q;
-      abase[h] = (lg >> 1) * KB * 1024 + (CI / 2) * wp * 1024 + (pp >> 1) * 256 + (((row & 15) ^ ((pp >> 1) * 12)) << 4) +
-                 (pp & 1) * 8;
-      bbase[h] = dv_rbgr(row, 2 * wn + (pp >> 1)) + 8 * (pp & 1);
-    }
-    const float cg = sgb[0][16 * wn + lr], cb = sgb[1][16 * wn + lr];
-    const float bal = p.bop.alpha[0];
-    auto run = [&](auto le1) __attribute__((always_inline)) {
-      constexpr bool LE1 = decltype(le1)::value;
-      int slot = 0;
-      uint32_t gen = 1;
-      DV_TS(tl0);
-      for (int t = t0; t < t1; ++t) {
-        DV_TS(tw0);
-        dv_wait<4>(fl_full[slot], gen, p.err);
-        DV_ACC(0, tw0);
-        const char* base = smem + slot * SLOT;
-        const s16x4_t lo = dv_tr(base + OFF_B + bbase[0]);
-        const s16x4_t hi = dv_tr(base + OFF_B + bbase[1]);
-        v4u v = __builtin_bit_cast(v4u, bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
-        {
-          const float2 st = *reinterpret_cast<const float2*>(base + OFF_ST);
-#pragma unroll
-          for (int kk = 0; kk < 4; ++kk) {
-            float x0 = __uint_as_float(v[kk] << 16), x1 = __uint_as_float(v[kk] & 0xffff0000u);
-            x0 = dv_prelu<LE1>(x0, bal);
-            x1 = dv_prelu<LE1>(x1, bal);
-            x0 = fmaf(x0 - st.x, st.y * cg, cb);
-            x1 = fmaf(x1 - st.x, st.y * cg, cb);
-            v[kk] = pk_bf16(x0, x1);
-          }
-        }
-        const bf16x8_t bfr = __builtin_bit_cast(bf16x8_t, v);
-#pragma unroll
-        for (int i = 0; i < CI; ++i) {
-          const int o = (i >> 1) * 1024 + (i & 1) * 512;
-          const s16x4_t alo = dv_tr(base + OFF_A + abase[0] + o), ahi = dv_tr(base + OFF_A + abase[1] + o);
-          dacc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              bf16x8_t{alo[0], alo[1], alo[2], alo[3], ahi[0], ahi[1], ahi[2], ahi[3]}, bfr, dacc[i], 0, 0, 0);
-        }
-        dv_signal(&fl_done[slot][NR + c], gen);
-        if (++slot == NSL) {
-          slot = 0;
-          ++gen;
-        }
-      }
-      DV_ACC(3, tl0);
-    };
-    if (bal <= 1.f) run(std::true_type{});
-    else run(std::false_type{});
-    DV_STAMP_STORE;
-    float* Dp = p.Dpart + (size_t)rr * KR * p.Nout;
-    const int n = n0 + 16 * wn + lr;
-#pragma unroll
-    for (int i = 0; i < CI; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        st_part<CTN_PART_NT != 0>(&Dp[(size_t)((wp * CI + i) * 16 + 4 * lg + e) * p.Nout + n], dacc[i][e]);
-    return;
-  }
-
-  // ======================= memory waves (+ row wave mw's epilogue) =======================
-  dv_prio<4, NORM_GLN>();
-  const int mw = wid - ND;
-  DV_STAMP_DECL;
-  const rsrc_t rA = du_rsrc(p.A, rows * p.lda * 2), rD = du_rsrc(p.Bm, rows * p.ldb * 2);
-  const rsrc_t rS = du_rsrc(p.bop.stats, (long)p.g.M * 8);
-  int arow[4];
-  uint32_t aoff[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int f = 4 * mw + u, mb = f / KB, kb = f % KB;
-    arow[u] = 16 * mb + ((lane & 15) ^ (((lane >> 4) & 1) * 12));
-    aoff[u] = (uint32_t)(arow[u] * p.lda + (4 * kb + (lane >> 4)) * 8) * 2u;
-  }
-  uint32_t doff[2];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int drow = 4 * (2 * mw + h) + (lane >> 4), ps = lane & 15;
-    const int dgr = (ps & 1) | ((((ps >> 1) ^ dv_rbhash(drow)) & 7) << 1);
-    doff[h] = (uint32_t)(drow * p.ldb + n0 + 8 * dgr) * 2u;
-  }
-  const bool st_wave = mw == 0;
-  const uint32_t soff = lane < 2 ? (uint32_t)(lane * 4) : DU_OOB;
-  auto dma = [&](int t) __attribute__((always_inline)) {
-    char* base = smem + ((t - t0) % NSL) * SLOT;
-    const int tk = (t * TM) % Kp;
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      du_dma16(rA, base + OFF_A + (4 * mw + u) * 1024, tk + arow[u] < Kv ? aoff[u] : DU_OOB, t * TM * p.lda * 2);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) du_dma16(rD, base + OFF_B + (2 * mw + h) * 1024, doff[h], t * TM * p.ldb * 2);
-    if (st_wave) du_dma4(rS, base + OFF_ST, soff, (t / tpu) * 8);
-  };
-  // row wave mw's epilogue state (its lane (lg, lr) holds channels 32 mw + 8 lg .. +7 of
-  // frame rows lr, 16 + lr)
-  const int cl = 32 * mw + 8 * lg;
-  bf16raw* Cg = reinterpret_cast<bf16raw*>(p.C);
-  float gamr[8];
-  *reinterpret_cast<float4*>(gamr) = *reinterpret_cast<const float4*>(p.gamma + n0 + cl);
-  *reinterpret_cast<float4*>(gamr + 4) = *reinterpret_cast<const float4*>(p.gamma + n0 + cl + 4);
-  const int ro = OFF_B + dv_rbgr(lr, 4 * mw + lg);
-  const float eal = p.alpha[0];
-  double run_s = 0.0, run_q = 0.0;
-  const int m0 = t0 / tpu;
-  int run_m = m0;
-  double2* run_slab = p.grp_slab + (((size_t)rr * S + sl) * DV_NR + mw) * kmax;
-  auto flush = [&]() __attribute__((always_inline)) {
-    const double s = wave_sum_dpp_d(run_s), ss = wave_sum_dpp_d(run_q);
-    run_slab[run_m - m0] = make_double2(s, ss);
-  };
-  // tile k = t - t0: the row wave's staged accumulators, raw d and statistics of its slot
-  auto epilogue = [&](auto le1, int t, int k) __attribute__((always_inline)) {
-    constexpr bool LE1 = decltype(le1)::value;
-    const int eb = k & 1;
-    DV_TS(ta0);
-    dv_wait1(&fl_acc[eb][mw], (uint32_t)(k >> 1) + 1u, p.err);
-    DV_ACC(0, ta0);
-    const char* base = smem + (k % NSL) * SLOT;
-    const float* E = &estage[eb][mw][0];
-    f32x4_t acc[2][2];
-#pragma unroll
-    for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-      for (int nb = 0; nb < 2; ++nb) acc[rb][nb] = *reinterpret_cast<const f32x4_t*>(E + (2 * rb + nb) * 256 + lane * 4);
-    const float2 est = *reinterpret_cast<const float2*>(base + OFF_ST);   // the tile's utterance
-    const float rs = est.y, ms = -est.x * est.y;
-    float s1[2] = {0.f, 0.f}, q1[2] = {0.f, 0.f};
-#pragma unroll
-    for (int rb = 0; rb < 2; ++rb) {
-      const v4u rw = *reinterpret_cast<const v4u*>(base + ro + rb * 4096);
-      float f[8];
-      unpack_bf16x8(rw, f);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float a = dv_prelu<LE1>(f[e], eal);
-        const float ah = fmaf(a, rs, ms);
-        const float ga = acc[rb][e >> 2][e & 3] * gamr[e];
-        s1[rb] += ga;
-        q1[rb] = fmaf(ga, ah, q1[rb]);
-      }
-      const v4u cv = {pk_bf16(acc[rb][0][0], acc[rb][0][1]), pk_bf16(acc[rb][0][2], acc[rb][0][3]),
-                      pk_bf16(acc[rb][1][0], acc[rb][1][1]), pk_bf16(acc[rb][1][2], acc[rb][1][3])};
-      stg16h<CTN_DV_NT != 0>(Cg + (size_t)t * TM * p.ldc + n0 + (uint32_t)((16 * rb + lr) * p.ldc + cl), cv);
-    }
-    const int m = t / tpu;
-    if (m != run_m) {
-      flush();
-      run_s = run_q = 0.0;
-      run_m = m;
-    }
-    run_s += (double)(s1[0] + s1[1]);
-    run_q += (double)(q1[0] + q1[1]);
-    dv_signal(&fl_efree[eb][mw], (uint32_t)(k >> 1) + 1u);
-    dv_signal(&fl_done[k % NSL][mw], (uint32_t)(k / NSL) + 1u);
-  };
-  auto run = [&](auto le1) __attribute__((always_inline)) {
-    for (int i = 0; i < PF; ++i)
-      if (t0 + i < t1) dma(t0 + i);
-    int slot = 0;
-    uint32_t gen = 1;
-    DV_TS(tl0);
-    for (int t = t0; t < t1; ++t) {
-      const int k = t - t0;
-      const int later = t1 - 1 - t < PF - 1 ? t1 - 1 - t : PF - 1;
-      // tile t's DMA group landed.  Issued after it: the PF - 1 later groups and, from
-      // k = PF on, one epilogue (2 C stores) per iteration in between (vmcnt counts loads
-      // and stores in issue order); before that the store-free count, which waits longer
-      DV_TS(tv0);
-      if (later == PF - 1) {
-        if (k >= PF + 1) {
-          if (st_wave) dv_vmwait_c<7 * (PF - 1) + 2 * PF>();
-          else dv_vmwait_c<6 * (PF - 1) + 2 * PF>();
-        } else {
-          if (st_wave) dv_vmwait_c<7 * (PF - 1)>();
-          else dv_vmwait_c<6 * (PF - 1)>();
-        }
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      DV_ACC(1, tv0);
-      dv_signal(&fl_full[slot][mw], gen);
-      // refill the slot of tile k + PF - NSL (<= k - 2: its epilogue ran last iteration)
-      const int tn = t + PF;
-      if (tn < t1) {
-        const int kn = tn - t0;
-        DV_TS(td0);
-        dv_wait<ND>(fl_done[kn % NSL], (uint32_t)(kn / NSL), p.err);
-        DV_ACC(2, td0);
-        dma(tn);
-      }
-      if (k >= 1) epilogue(le1, t - 1, k - 1);
-      if (++slot == NSL) {
-        slot = 0;
-        ++gen;
-      }
-    }
-    epilogue(le1, t1 - 1, t1 - 1 - t0);
-    DV_ACC(3, tl0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  };
-  if (t0 < t1) {
-    if (eal <= 1.f) run(std::true_type{});
-    else run(std::false_type{});
-    flush();
-  }
-  DV_STAMP_STORE;
-}
-
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -1575,27 +919,12 @@ bool gemm_dual_ws_enabled() {
 // cLN statistics entries per (row, slice) the kernel stores (gemm_dual_group_parts)
 int dual_ws_cln_parts_per_slice() { return CTN_DV_CLNC ? 1 : DV_NR; }
 
-// The gLN form on gemm_dual_r8_kernel (eight row waves, the tile DMA in the column
-// waves): CTN_DUAL_R8=1 (experiment; read on every query).  Bit-identical C and dW2, but
-// measured slower: 95-120 us against 75-79 us for the four-row-wave kernel at the bench
-// shape (microbenchmark, round 6) — without dedicated high-priority memory
-// waves the DMA issue waits behind the column waves' MFMA work and the ring runs dry.
-static bool dual_r8(const GemmDual& p) {
-  if (p.norm != NORM_GLN) return false;
-  const char* e = getenv("CTN_DUAL_R8");
-  return e ? atoi(e) != 0 : false;
-}
-// row waves per slice of the wave-specialised kernel that runs p (its gLN statistics
-// partials are per (range, slice, row wave): gemm_dual_runs)
-int dual_ws_row_waves(const GemmDual& p) { return dual_r8(p) ? 8 : DV_NR; }
-
-// The gLN form on gemm_dual_me_kernel (the row epilogue in the memory waves):
-// CTN_DUAL_ME=1 (read on every query).  Bit-identical C, dW2 and statistics.
-static bool dual_me(const GemmDual& p) {
-  if (!DV_ME_OK || p.norm != NORM_GLN) return false;
-  const char* e = getenv("CTN_DUAL_ME");
-  return e ? atoi(e) != 0 : false;
-}
+// row waves per slice of the wave-specialised kernel (its gLN statistics partials are per
+// (range, slice, row wave): gemm_dual_runs).  Round 6 measured two other gLN forms, both
+// bit-identical and slower, and removed them: eight row waves with the
+// tile DMA in the column waves (commit 9656623) and the row epilogue in the memory waves
+// (commit 9d56d29).
+int dual_ws_row_waves(const GemmDual&) { return DV_NR; }
 
 bool gemm_dual_ws_eligible(const GemmDual& p) {
   if (!gemm_dual_ws_enabled()) return false;
@@ -1662,12 +991,7 @@ hipError_t launch_gemm_dual_ws(const GemmDual& pa, hipStream_t s) {
   GemmDual p = pa;
   p.err = device_error_word();
   const dim3 grid(gemm_dual_ws_ranges(p) * (p.Nout / DV_NS));
-  if (p.norm == NORM_GLN && dual_r8(p))
-    hipLaunchKernelGGL((gemm_dual_r8_kernel<DV_NSL, DV_PF>), grid, dim3(1024), 0, s, p);
-  else if (dual_me(p)) {
-    if constexpr (DV_ME_OK) hipLaunchKernelGGL((gemm_dual_me_kernel<CTN_DVM_NSL, CTN_DVM_PF>), grid, dim3(DV_NT), 0, s, p);
-  }
-  else if (p.norm == NORM_GLN)
+  if (p.norm == NORM_GLN)
     hipLaunchKernelGGL((gemm_dual_ws_kernel<NORM_GLN, DV_NSL, DV_PF>), grid, dim3(DV_NT), 0, s, p);
   else
     hipLaunchKernelGGL((gemm_dual_ws_kernel<NORM_CLN, DV_NSL, DV_PF_CLN>), grid, dim3(DV_NT), 0, s, p);
