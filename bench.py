@@ -538,7 +538,7 @@ def main():
         if os.path.exists(pmc) and args.config == "c2" and not args.fp32:
             with open(pmc) as f:
                 step_pmc = json.load(f).get("step_GB")
-        pmc = os.path.join(ROOT, "profiles", "pmc_mfma.json")   # tools/gpu_round2.sh MFMA pass
+        pmc = os.path.join(ROOT, "profiles", "pmc_mfma.json")   # tools/gpu.sh prof, MFMA pass
         if os.path.exists(pmc):
             with open(pmc) as f:
                 mfma = json.load(f).get(str(args.timer_kind))

@@ -23,7 +23,7 @@ mkdir -p "$O"
 ROOT=$(pwd)
 
 line() {   # the bench JSON line's headline fields
-  tail -1 "$1" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print(d['value'], d['ms_per_step'], 'frac', r['frac'], 'mean_ms', r['mean_ms'], r['kernel'][:40])"
+  grep '^{' "$1" | tail -1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print(d['value'], d['ms_per_step'], 'frac', r['frac'], 'mean_ms', r['mean_ms'], r['kernel'][:40])"
 }
 
 case $cmd in
