@@ -232,7 +232,8 @@ class FlatGradAllReduce:
         idx = {id(p): i for i, p in enumerate(self.params)}
         desc = [(ai, [idx[id(p)] for p in g[a:b]]) for ai, (g, _, _, chunks) in enumerate(self._arenas)
                 for a, b, _, _ in chunks]
-        return int.from_bytes(hashlib.sha1(repr(desc).encode()).digest()[:8], "little", signed=True)
+        # 62 bits, non-negative: -h below stays inside int64
+        return int.from_bytes(hashlib.sha1(repr(desc).encode()).digest()[:8], "little") >> 2
 
     def _check_layout(self):
         """Every rank must issue the same all-reduce sequence: compare the layout hashes
