@@ -229,7 +229,7 @@ class Adam(torch.optim.Optimizer):
                         maximize=False, foreach=None, capturable=bool(capturable), differentiable=False,
                         fused=None)
         super().__init__(params, defaults)
-        # capturable groups: device step counter and bias-correction table per group
+        # capturable groups: device step counter and lr per group (_capture_state)
         self._cap: dict = {}
         self._plans: OrderedDict = OrderedDict()
         self._steps: dict = {}   # param -> int step (mirrored into state['step'] lazily)
